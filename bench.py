@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X MapCrdt merge hot path (BASELINE.json metric).
+
+Metric: merged records/sec (whole job, all ranks) on the 1024-replica fan-in
+workload — 1B records, Zipf(0.8) keys over 2^28 ids, a 2^27-key local map —
+plus the HBM-roofline fraction of the dominant kernel (K2 apply) and of the
+whole job.  One "step" = one crdt_merge of the whole batch (R = 1024 sequential
+Crdt.merge calls, crdt.dart:77-94) with every input already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+N > 1: keys are sharded by key % N (strong scaling: the total stays 1B);
+changeset j is homed on rank j % N for the canonical-clock scan; the per-
+changeset maxima and the first-exception word are combined with RCCL
+all-reduces (torch.distributed "nccl" = RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", choices=["fanin", "cfg2"], default="fanin")
+    p.add_argument("--records", type=int, default=1_000_000_000)
+    p.add_argument("--replicas", type=int, default=1024)
+    p.add_argument("--keys", type=int, default=1 << 28)
+    p.add_argument("--local", type=int, default=1 << 27)
+    p.add_argument("--zipf", type=float, default=0.8)
+    p.add_argument("--order", choices=["shuffled", "ascending"], default="shuffled")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_cfg2, gen_fanin
+
+    t0 = time.time()
+    if args.config == "fanin":
+        wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                       device=dev, order=args.order, rank=rank, world=world)
+        workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
+                    f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
+                    f"{args.order} order), local map 2^{int(np.log2(args.local))} keys, keys sharded key%N")
+    else:
+        assert world == 1, "cfg2 is a single-GPU configuration"
+        wl = gen_cfg2(device=dev)
+        workload = "cfg2: 10M-key local map + one 10M-record changeset, ~50% key overlap"
+    torch.cuda.synchronize()
+    log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
+
+    table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
+    loc = wl["local"]
+    own, home = wl["owned"], wl["home"]
+    own_cols = (own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], None)
+    home_cols = (own["key"][:0] if world > 1 else own["key"], home["lt"], home["rank"],
+                 own["val"][:0] if world > 1 else own["val"], wl["home_offsets"], None)
+    R = wl["R"]
+    d_max = torch.zeros(max(R, 1), dtype=torch.int64, device=dev)
+    d_ev = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def reset():
+        table.clear_rows(0, wl["capacity"])
+        table.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        table.canonical = wl["c0"]
+        torch.cuda.synchronize()
+
+    def step(flags=None):
+        if world == 1:
+            res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
+            return res
+        # key-sharded: home scan -> MAX(M_j) -> clock -> MIN(event) -> resolve -> MAX(details) -> apply
+        table.merge_scan(home_cols, wl["wall"], d_max)
+        dist.all_reduce(d_max.view(torch.uint64) if hasattr(torch, "uint64") else d_max, op=dist.ReduceOp.MAX)
+        table.merge_clock(home_cols, wl["wall"], d_max, d_ev)
+        ev0 = d_ev[:1]
+        dist.all_reduce(ev0.view(torch.uint64) if hasattr(torch, "uint64") else ev0, op=dist.ReduceOp.MIN)
+        table.merge_resolve(home_cols, d_ev)
+        rest = d_ev[1:]
+        dist.all_reduce(rest.view(torch.uint64) if hasattr(torch, "uint64") else rest, op=dist.ReduceOp.MAX)
+        torch.cuda.synchronize()
+        return table.merge_apply(own_cols, wl["wall"], d_ev, win_flags=flags)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        reset()
+        step()
+    table.set_timing(True)
+    step_ms, apply_ms, apply_launches, scan_ms = [], 0.0, 0, 0.0
+    res = None
+    for _ in range(args.steps):
+        reset()
+        barrier()
+        ts = time.perf_counter()
+        res = step()
+        barrier()
+        dt = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        step_ms.append(dt * 1e3)
+        tm = table.timing()
+        apply_ms += tm["apply_ms"]
+        apply_launches += tm["apply_launches"]
+        scan_ms += tm["scan_ms"]
+    table.set_timing(False)
+    assert res["status"] == 0, res
+    ms_per_step = float(np.mean(step_ms))
+    total_records = wl["total"]
+    value = total_records / (ms_per_step / 1e3)
+
+    # ---- per-kernel roofline of K2 (apply): algorithmic bytes / event-timed duration
+    n_owned = int(wl["owned_offsets"][-1])
+    kb = 20 * n_owned + 12 * res["n_present"] + 24 * res["n_won"]          # per step, this rank
+    achieved = kb * args.steps / (apply_ms / 1e3) if apply_ms > 0 else 0.0
+    avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)
+    roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                "kernel": "k_apply (K2)", "avg_launch_us": round(avg_launch_us, 2),
+                "alg_bytes_per_launch": int(kb / max(apply_launches // max(args.steps, 1), 1))}
+    # traffic (PMC) is filled from the committed rocprofv3 --pmc pass of this command, when present
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_apply.json")
+    if os.path.exists(pmc) and world == 1 and args.config == "fanin":
+        try:
+            roofline["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ---- whole-job algorithmic bytes: distinct keys touched / won (one untimed census run)
+    job = {}
+    if not args.no_census and world == 1:
+        reset()
+        flags = torch.zeros(max(n_owned, 1), dtype=torch.uint8, device=dev)
+        r2 = step(flags=flags) if world == 1 else None
+        keys = own["key"]
+        won_keys = torch.unique(keys[flags[:n_owned].bool()])
+        all_keys = torch.unique(keys)
+        u_touch = int((all_keys < wl["n_local_rows"]).sum().item()) if args.config == "fanin" else \
+            int((all_keys < wl["n_local"]).sum().item())
+        u_win = int(won_keys.numel())
+        b_alg = 20 * total_records + 12 * u_touch + 24 * u_win
+        job = {"U_touch": u_touch, "U_win": u_win, "B_alg_bytes": b_alg,
+               "hbm_frac_job": round(b_alg / (ms_per_step / 1e3) / HBM_PEAK, 4),
+               "records_won_total": int(r2["n_won"])}
+        del flags, won_keys, all_keys
+
+    # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(wl, args.cpu_seconds)
+
+    out = {
+        "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
+        "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "config": {"workload": workload, "records": total_records, "replicas": R,
+                   "parallelism": f"keyshard{world}" if world > 1 else "single",
+                   "step_ms_all": [round(x, 3) for x in step_ms]},
+        "roofline": roofline, "job": job, "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    table.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(wl, budget_s):
+    """Times oracle/merge_oracle.c (faithful port: map copy per merge + clock read per record,
+    single thread) on the first changesets of the same workload, within ~budget_s seconds."""
+    import torch
+    from oracle.oracle_c import OracleTable
+    loc = wl["local"]
+    cap = wl["capacity"]
+    t = OracleTable(cap, 0, wl["c0"])
+    t.put_rows(loc["slot"].cpu().numpy().astype(np.uint32), loc["lt"].cpu().numpy(),
+               loc["rank"].cpu().numpy().astype(np.uint32), loc["val"].cpu().numpy().astype(np.uint32),
+               loc["mod"].cpu().numpy())
+    offs = wl["owned_offsets"]
+    own = wl["owned"]
+    done, recs, el = 0, 0, 0.0
+    rows_copied = 0
+    while done < wl["R"] and el < budget_s:
+        b, e = int(offs[done]), int(offs[done + 1])
+        sl = slice(b, e)
+        cols = [own[k][sl].cpu().numpy() for k in ("key", "lt", "rank", "val")]
+        ts = time.perf_counter()
+        res, _ = t.merge(cols[0].astype(np.uint32), cols[1], cols[2].astype(np.uint32),
+                         cols[3].astype(np.uint32), np.array([0, e - b], np.uint64), wl["wall"], faithful=True,
+                         want_flags=False)
+        el += time.perf_counter() - ts
+        done += 1
+        recs += e - b
+        rows_copied += cap
+    del t
+    torch.cuda.synchronize()
+    return {"value": round(recs / el, 1), "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged into the full "
+                      f"{cap:,}-row map by oracle/merge_oracle.c in faithful mode (one full map copy per "
+                      f"merge, map_crdt.dart:43; one clock read per record, hlc.dart:82), {el:.1f}s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+"""ctypes binding of ``include/crdt_merge.h`` (``crdt_amd/libcrdt_mi355x.so``).
+
+The shared library is the only compute path: if it is missing, or there is no
+gfx950 device, every operation raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcrdt_mi355x.so")
+
+CRDT_OK = 0
+CRDT_CLOCK_DRIFT = 1
+CRDT_DUPLICATE_NODE = 2
+CRDT_OVERFLOW = 3
+CRDT_E_INVALID = -1
+CRDT_E_HIP = -2
+CRDT_E_NOMEM = -3
+CRDT_E_KEY_RANGE = -4
+CRDT_E_NO_DEVICE = -5
+
+CRDT_MEM_HOST = 0
+CRDT_MEM_DEVICE = 1
+CRDT_NULL_VALUE = 0xFFFFFFFF
+
+
+class CrdtBatch(ctypes.Structure):
+    _fields_ = [("key_id", ctypes.c_void_p), ("lt", ctypes.c_void_p), ("rank", ctypes.c_void_p),
+                ("val", ctypes.c_void_p), ("millis", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("n_changesets", ctypes.c_uint32), ("mem", ctypes.c_int32)]
+
+
+class CrdtResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("n_stored", ctypes.c_uint32),
+                ("exc_changeset", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("exc_index", ctypes.c_uint64), ("canonical_lt", ctypes.c_int64),
+                ("drift_ms", ctypes.c_int64), ("counter", ctypes.c_int64),
+                ("n_present", ctypes.c_uint64), ("n_won", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class CrdtTiming(ctypes.Structure):
+    _fields_ = [("scan_ms", ctypes.c_double), ("clock_ms", ctypes.c_double),
+                ("apply_ms", ctypes.c_double), ("apply_launches", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("total_ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_INT = ctypes.c_int
+
+# name -> (restype, argtypes); exactly the entry points include/crdt_merge.h declares
+SIGNATURES = {
+    "crdt_abi_version": (_INT, []),
+    "crdt_status_string": (ctypes.c_char_p, [_INT]),
+    "crdt_device_count": (_INT, [_P]),
+    "crdt_create": (_INT, [_INT, _U32, _U64, _P]),
+    "crdt_destroy": (None, [_P]),
+    "crdt_reserve": (_INT, [_P, _U64]),
+    "crdt_capacity": (_INT, [_P, _P]),
+    "crdt_set_local_rank": (_INT, [_P, _U32]),
+    "crdt_get_canonical": (_INT, [_P, _P]),
+    "crdt_set_canonical": (_INT, [_P, _I64]),
+    "crdt_put_rows": (_INT, [_P, _P, _P, _P, _P, _P, _U64, _I32]),
+    "crdt_read_rows": (_INT, [_P, _P, _U64, _P, _P, _P, _P, _I32]),
+    "crdt_modified_since": (_INT, [_P, _U64, _I64, _P, _P]),
+    "crdt_clear_rows": (_INT, [_P, _U64, _U64]),
+    "crdt_remap_ranks": (_INT, [_P, _U64, _P, _U32]),
+    "crdt_put_stamped": (_INT, [_P, _P, _P, _U64, _I64, _I32, _P]),
+    "crdt_refresh_canonical": (_INT, [_P, _U64, _P]),
+    "crdt_merge": (_INT, [_P, _P, _I64, _P, _P]),
+    "crdt_merge_scan": (_INT, [_P, _P, _I64, _P]),
+    "crdt_merge_clock": (_INT, [_P, _P, _I64, _P, _P]),
+    "crdt_merge_resolve": (_INT, [_P, _P, _P]),
+    "crdt_merge_apply": (_INT, [_P, _P, _I64, _P, _P, _P]),
+    "crdt_set_timing": (_INT, [_P, _INT]),
+    "crdt_get_timing": (_INT, [_P, _P]),
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load the gfx950 library (raises loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def status_string(status: int) -> str:
+    return load().crdt_status_string(status).decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load().crdt_device_count(ctypes.byref(n))
+    return n.value

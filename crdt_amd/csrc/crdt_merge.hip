@@ -1,0 +1,1287 @@
+// crdt_merge.hip — MI355X (gfx950) implementation of the MapCrdt merge hot path.
+//
+// Implements include/crdt_merge.h.  The reference is the Dart package `crdt`
+// v4.0.2 (/root/reference); every kernel names the reference lines it replaces.
+// DESIGN.md has the data layout, the roofline of each kernel and the proof that
+// the batched clock algebra below equals R sequential Crdt.merge() calls.
+//
+// Kernels (one HIP stream per ctx; every call is synchronous at the API edge):
+//   K3a k_scan     per-changeset max lt (M_j) + tiles holding a record that can
+//                  raise (Hlc.recv, hlc.dart:80-97)            [HBM stream, 12 B/record]
+//   K3b k_clock    one workgroup: canonical recurrence C_j = send(max(C_{j-1}, M_j))
+//                  as a prefix max; R_j stamps; first send() failure (hlc.dart:51-74)
+//   K3c k_verify   exact first recv() failure inside candidate tiles (ordered
+//                  wave scan), only when a candidate exists (rare)
+//   K3d k_resolve  stop point, status and final canonical (single thread)
+//   K2  k_apply    per changeset: gather the local row, (lt, rank) compare, store
+//                  winner {lt, rank, val, mod = R_j} (crdt.dart:83-90)
+//                  [HBM: 20 B/record stream + 32 B row gather/scatter]
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "crdt_merge.h"
+
+namespace {
+
+constexpr int kShift = 16;                       // hlc.dart:3
+constexpr int64_t kMaxCounter = 0xFFFF;          // hlc.dart:4
+constexpr int64_t kMaxDrift = 60000;             // hlc.dart:5
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kTile = kScanThreads * kScanItems; // 4096 records per scan tile
+constexpr int kApplyThreads = 256;
+constexpr int kApplyItems = 4;
+constexpr int kApplyPerBlock = kApplyThreads * kApplyItems;
+constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
+constexpr int kVerifyBlocks = 64;
+
+constexpr uint64_t kLowBits = 40;
+constexpr uint64_t kLowMask = (1ull << kLowBits) - 1;  // event low word == kLowMask: send() failure
+constexpr uint64_t kEvNone = ~0ull;
+constexpr uint64_t kSign = 1ull << 63;
+
+// One device row per key id.  32-byte aligned: a random access is one 32-B sector.
+struct alignas(32) Row {
+    int64_t lt;      // Record.hlc.logicalTime
+    uint32_t rank;   // Record.hlc.nodeId rank
+    uint32_t val;    // Record.value handle
+    int64_t mod;     // Record.modified.logicalTime (< 0: invisible to merge / recordMap)
+    int64_t aux;     // reserved (zero)
+};
+static_assert(sizeof(Row) == 32, "row layout");
+
+// Device-side per-call words.
+struct Misc {
+    uint32_t cand_count;   // candidate tiles appended by k_scan
+    uint32_t stop;         // changesets to apply (set by k_resolve)
+    uint32_t err;          // key range violation
+    uint32_t pad;
+    crdt_result result;    // filled by k_resolve
+    unsigned long long present[kCounterSlots];
+    unsigned long long won[kCounterSlots];
+};
+
+__host__ __device__ inline unsigned long long enc(int64_t x) { return (unsigned long long)x ^ kSign; }
+__host__ __device__ inline int64_t dec(unsigned long long u) { return (int64_t)(u ^ kSign); }
+__host__ __device__ inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+__host__ __device__ inline int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
+
+// ------------------------------------------------------------------ wave helpers
+__device__ inline int64_t wave_max(int64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = imax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+__device__ inline int64_t wave_scan_max_incl(int64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int64_t u = __shfl_up(v, off, 64);
+        if (lane >= off) v = imax(v, u);
+    }
+    return v;
+}
+
+// =============================================================================
+// K3a — k_scan: M_j = max lt of changeset j; tiles that may raise in recv().
+// A record can raise only if it is flagged (rank == local: DuplicateNode,
+// hlc.dart:88-90; millis - wall > 60000: ClockDrift, hlc.dart:92-94) AND its lt
+// exceeds the canonical; canonicals never decrease, so lt <= C_0 can never raise.
+// =============================================================================
+__global__ __launch_bounds__(kScanThreads) void k_scan(
+    const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
+    int64_t wall, uint32_t local_rank, unsigned long long* __restrict__ M,
+    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
+{
+    __shared__ int64_t s_max[kScanThreads / 64];
+    __shared__ int s_flag[kScanThreads / 64];
+    const uint32_t j = jbase + blockIdx.y;
+    const uint64_t beg = offs[j], end = offs[j + 1];
+    const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint64_t base = beg + (uint64_t)t * kTile;
+        int64_t m = INT64_MIN;
+        int f = 0;
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            if (i < end) {
+                const int64_t v = lt[i];
+                const uint32_t r = rank[i];
+                const int64_t ms = millis ? millis[i] : (v >> kShift);
+                m = imax(m, v);
+                f |= (v > c0) & ((r == local_rank) | (wsub(ms, wall) > kMaxDrift));
+            }
+        }
+        m = wave_max(m);
+        const int fw = __any(f);
+        if (lane == 0) { s_max[w] = m; s_flag[w] = fw; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tm = s_max[0];
+            int tf = s_flag[0];
+            for (int k = 1; k < kScanThreads / 64; ++k) { tm = imax(tm, s_max[k]); tf |= s_flag[k]; }
+            T[t0 + t] = tm;
+            atomicMax(&M[j], enc(tm));
+            if (tf) {
+                const uint32_t c = atomicAdd(&misc->cand_count, 1u);
+                cand_tile[c] = t0 + t;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// =============================================================================
+// K3b — k_clock (one workgroup).  Sequential merges give (crdt.dart:82, 93)
+//   R_j = max(C_{j-1}, M_j)               canonical after the recv loop
+//   C_j = send(R_j) = max(R_j + 1, W)     W = wall << 16   (hlc.dart:51-74)
+// so D_j = C_j - j = max(C_0, max_{k<=j}(max(M_k + 1, W) - k)) — a prefix max.
+// Also finds the first changeset whose send() raises (drift, then overflow).
+// =============================================================================
+__device__ inline bool send_fails(int64_t r, int64_t wall) {
+    const int64_t m = r >> kShift, c = r & kMaxCounter;
+    const int64_t mn = imax(m, wall);
+    const int64_t cn = (m == mn) ? c + 1 : 0;
+    return wsub(mn, wall) > kMaxDrift || cn > kMaxCounter;
+}
+
+__global__ __launch_bounds__(1024) void k_clock(
+    const unsigned long long* __restrict__ M, uint32_t R, int64_t wall, int64_t c0,
+    int64_t* __restrict__ Cprev, int64_t* __restrict__ Rj, int64_t* __restrict__ Cj,
+    unsigned long long* __restrict__ event)
+{
+    __shared__ int64_t s_wave[16];
+    __shared__ uint32_t s_first;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t W = (int64_t)((uint64_t)wall << kShift);
+    int64_t carry = c0;                       // D_0 = C_0
+    uint32_t first = UINT32_MAX;
+    if (tid == 0) s_first = UINT32_MAX;
+    __syncthreads();
+    for (uint32_t base = 0; base < R; base += 1024) {
+        const uint32_t j = base + tid;
+        const bool valid = j < R;
+        const int64_t jj = (int64_t)j + 1;
+        const int64_t mj = valid ? dec(M[j]) : INT64_MIN;
+        const bool has = mj != INT64_MIN;
+        const int64_t b = has ? imax(mj + 1, W) : W;
+        const int64_t key = valid ? b - jj : INT64_MIN;
+        int64_t incl = wave_scan_max_incl(key, lane);
+        if (lane == 63) s_wave[w] = incl;
+        __syncthreads();
+        if (w == 0) {
+            int64_t x = lane < 16 ? s_wave[lane] : INT64_MIN;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                int64_t u = __shfl_up(x, off, 64);
+                if (lane >= off) x = imax(x, u);
+            }
+            if (lane < 16) s_wave[lane] = x;
+        }
+        __syncthreads();
+        const int64_t wprev = w > 0 ? s_wave[w - 1] : INT64_MIN;
+        int64_t excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = INT64_MIN;
+        excl = imax(excl, wprev);
+        incl = imax(incl, wprev);
+        const int64_t total = s_wave[15];
+        const int64_t cprev = imax(carry, excl) + (jj - 1);
+        const int64_t ccur = imax(carry, incl) + jj;
+        if (valid) {
+            const int64_t r = has ? imax(cprev, mj) : cprev;
+            Cprev[j] = cprev;
+            Rj[j] = r;
+            Cj[j] = ccur;
+            if (send_fails(r, wall)) first = first < j ? first : j;
+        }
+        carry = imax(carry, total);
+        __syncthreads();
+    }
+    if (first != UINT32_MAX) atomicMin(&s_first, first);
+    __syncthreads();
+    if (tid == 0 && s_first != UINT32_MAX)
+        atomicMin(event, ((unsigned long long)s_first << kLowBits) | kLowMask);
+}
+
+// =============================================================================
+// K3c — k_verify: for each candidate tile, the first record i (in iteration
+// order) with flag(i) && lt_i > max(C_{j-1}, lt of every earlier record of j),
+// i.e. the first Hlc.recv that throws (hlc.dart:85-94).  One wave per tile,
+// ordered 64-record rounds with a shuffle prefix max.  Rare path.
+// =============================================================================
+__global__ __launch_bounds__(64) void k_verify(
+    const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ tstart, uint32_t R, const int64_t* __restrict__ T,
+    const int64_t* __restrict__ Cprev, int64_t wall, uint32_t local_rank,
+    const Misc* __restrict__ misc, const uint32_t* __restrict__ cand_tile,
+    unsigned long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
+    uint32_t* __restrict__ cand_kind, int64_t* __restrict__ cand_ms,
+    unsigned long long* __restrict__ event)
+{
+    const int lane = threadIdx.x;
+    const uint32_t n = misc->cand_count;
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const uint32_t gt = cand_tile[c];
+        uint32_t lo = 0, hi = R;                     // largest j with tstart[j] <= gt
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tstart[mid] <= gt) lo = mid; else hi = mid;
+        }
+        const uint32_t j = lo;
+        const uint32_t t = gt - tstart[j];
+        int64_t P = Cprev[j];
+        for (uint32_t u = tstart[j] + lane; u < gt; u += 64) P = imax(P, T[u]);
+        P = wave_max(P);
+        const uint64_t base = offs[j] + (uint64_t)t * kTile;
+        const uint64_t end = std::min<uint64_t>(base + kTile, offs[j + 1]);
+        bool found = false;
+        uint64_t fi = 0;
+        int64_t fp = 0, fms = 0;
+        uint32_t fkind = 0;
+        for (uint64_t i0 = base; i0 < end; i0 += 64) {
+            const uint64_t i = i0 + lane;
+            const bool in = i < end;
+            const int64_t v = in ? lt[i] : INT64_MIN;
+            const uint32_t r = in ? rank[i] : 0;
+            const int64_t ms = in ? (millis ? millis[i] : (v >> kShift)) : 0;
+            const bool dup = in && r == local_rank;
+            const bool drift = in && wsub(ms, wall) > kMaxDrift;
+            const int64_t incl = wave_scan_max_incl(v, lane);
+            int64_t excl = __shfl_up(incl, 1, 64);
+            if (lane == 0) excl = INT64_MIN;
+            excl = imax(excl, P);
+            const bool viol = (dup || drift) && v > excl;
+            const unsigned long long b = __ballot(viol);
+            if (b) {
+                const int L = __ffsll((long long)b) - 1;
+                fi = __shfl(i, L, 64);
+                fp = __shfl(excl, L, 64);
+                fms = __shfl(ms, L, 64);
+                fkind = __shfl(dup ? (uint32_t)CRDT_DUPLICATE_NODE : (uint32_t)CRDT_CLOCK_DRIFT, L, 64);
+                found = true;
+                break;
+            }
+            P = imax(P, __shfl(incl, 63, 64));
+        }
+        if (lane == 0) {
+            if (found) {
+                const unsigned long long key = ((unsigned long long)j << kLowBits) | (fi - offs[j]);
+                cand_key[c] = key;
+                cand_P[c] = fp;
+                cand_kind[c] = fkind;
+                cand_ms[c] = fms;
+                atomicMin(event, key);
+            } else {
+                cand_key[c] = kEvNone;
+            }
+        }
+    }
+}
+
+// Publish the recv-failure details of the global first event if this ctx holds
+// it: event[1] = enc(canonical at failure), event[2] = kind, event[3] = enc(millis).
+__global__ __launch_bounds__(256) void k_resolve_local(
+    const Misc* __restrict__ misc, const unsigned long long* __restrict__ cand_key,
+    const int64_t* __restrict__ cand_P, const uint32_t* __restrict__ cand_kind,
+    const int64_t* __restrict__ cand_ms, unsigned long long* __restrict__ event)
+{
+    const unsigned long long ev = event[0];
+    if (threadIdx.x == 0) { event[1] = 0; event[2] = 0; event[3] = 0; }
+    __syncthreads();
+    if (ev == kEvNone || (ev & kLowMask) == kLowMask) return;
+    const uint32_t n = misc->cand_count;
+    for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
+        if (cand_key[c] == ev) {
+            event[1] = enc(cand_P[c]);
+            event[2] = cand_kind[c];
+            event[3] = enc(cand_ms[c]);
+        }
+    }
+}
+
+// =============================================================================
+// K3d — k_resolve: stop point, status, final canonical (crdt.dart:80-93 order:
+// every recv of changeset j, then its store, then its send).
+// =============================================================================
+__global__ void k_resolve(const unsigned long long* __restrict__ event, uint32_t R, int64_t wall,
+                          int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
+                          Misc* __restrict__ misc)
+{
+    if (threadIdx.x != 0) return;
+    crdt_result res = {};
+    res.exc_index = UINT64_MAX;
+    const unsigned long long ev = event[0];
+    uint32_t stop;
+    if (ev == kEvNone) {
+        stop = R;
+        res.status = CRDT_OK;
+        res.canonical_lt = R ? Cj[R - 1] : c0;
+    } else {
+        const uint32_t j = (uint32_t)(ev >> kLowBits);
+        const uint64_t low = ev & kLowMask;
+        res.exc_changeset = j;
+        if (low == kLowMask) {                       // send() after storing changeset j
+            stop = j + 1;
+            const int64_t r = Rj[j];
+            const int64_t m = r >> kShift, c = r & kMaxCounter;
+            const int64_t mn = imax(m, wall);
+            res.canonical_lt = r;
+            if (wsub(mn, wall) > kMaxDrift) {
+                res.status = CRDT_CLOCK_DRIFT;
+                res.drift_ms = wsub(mn, wall);
+            } else {
+                res.status = CRDT_OVERFLOW;
+                res.counter = c + 1;
+            }
+        } else {                                     // recv() inside changeset j
+            stop = j;
+            res.exc_index = low;
+            res.canonical_lt = dec(event[1]);
+            res.status = (int32_t)event[2];
+            if (res.status == CRDT_CLOCK_DRIFT) res.drift_ms = wsub(dec(event[3]), wall);
+        }
+    }
+    res.n_stored = stop;
+    misc->stop = stop;
+    misc->result = res;
+}
+
+// =============================================================================
+// K2 — k_apply: one changeset (crdt.dart:83-90).  Winner <=> local absent
+// (mod < 0) or local.hlc < remote.hlc in (lt, rank) order; equal keeps local.
+// =============================================================================
+__global__ __launch_bounds__(kApplyThreads) void k_apply(
+    const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
+    const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
+    uint64_t end, uint32_t j, Row* __restrict__ table, uint64_t cap,
+    const int64_t* __restrict__ Rj, Misc* __restrict__ misc, uint8_t* __restrict__ flags)
+{
+    if (j >= misc->stop) return;
+    const int64_t stamp = Rj[j];
+    const uint64_t base = beg + (uint64_t)blockIdx.x * kApplyPerBlock;
+    uint32_t k[kApplyItems], r[kApplyItems], v[kApplyItems];
+    int64_t l[kApplyItems];
+    bool in[kApplyItems];
+#pragma unroll
+    for (int q = 0; q < kApplyItems; ++q) {
+        const uint64_t i = base + (uint64_t)q * kApplyThreads + threadIdx.x;
+        in[q] = i < end;
+        if (in[q]) {
+            k[q] = __builtin_nontemporal_load(key + i);
+            l[q] = __builtin_nontemporal_load(lt + i);
+            r[q] = __builtin_nontemporal_load(rank + i);
+            v[q] = __builtin_nontemporal_load(val + i);
+        }
+    }
+    uint4 a[kApplyItems], bq[kApplyItems];
+    bool ok[kApplyItems];
+#pragma unroll
+    for (int q = 0; q < kApplyItems; ++q) {
+        ok[q] = in[q] && k[q] < cap;
+        if (ok[q]) {
+            const uint4* p = reinterpret_cast<const uint4*>(table + k[q]);
+            a[q] = p[0];
+            bq[q] = p[1];
+        }
+    }
+    int npres = 0, nwon = 0;
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < kApplyItems; ++q) {
+        bool win = false;
+        if (ok[q]) {
+            const int64_t llt = (int64_t)(((uint64_t)a[q].y << 32) | a[q].x);
+            const uint32_t lrank = a[q].z;
+            const int64_t lmod = (int64_t)(((uint64_t)bq[q].y << 32) | bq[q].x);
+            const bool present = lmod >= 0;
+            win = !present || l[q] > llt || (l[q] == llt && r[q] > lrank);
+            npres += present;
+            if (win) {
+                uint4* p = reinterpret_cast<uint4*>(table + k[q]);
+                p[0] = make_uint4((uint32_t)l[q], (uint32_t)((uint64_t)l[q] >> 32), r[q], v[q]);
+                p[1] = make_uint4((uint32_t)stamp, (uint32_t)((uint64_t)stamp >> 32), 0u, 0u);
+                ++nwon;
+            }
+        } else if (in[q]) {
+            bad = true;
+        }
+        if (flags && in[q]) flags[base + (uint64_t)q * kApplyThreads + threadIdx.x] = win ? 1 : 0;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
+    // wave-level counts, one striped atomic per wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        npres += __shfl_xor(npres, off, 64);
+        nwon += __shfl_xor(nwon, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        const int slot = (blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6)) & (kCounterSlots - 1);
+        if (npres) atomicAdd(&misc->present[slot], (unsigned long long)npres);
+        if (nwon) atomicAdd(&misc->won[slot], (unsigned long long)nwon);
+    }
+}
+
+// ----------------------------------------------------------------- SPI kernels
+__global__ __launch_bounds__(256) void k_put_rows(
+    const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Row* __restrict__ table,
+    uint64_t cap, Misc* __restrict__ misc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    Row row;
+    row.lt = lt[i]; row.rank = rank[i]; row.val = val[i]; row.mod = mod[i]; row.aux = 0;
+    table[k] = row;
+}
+
+// put/putAll rows (crdt.dart:41-42, 51-53): hlc = modified = the one send() result.
+__global__ __launch_bounds__(256) void k_put_stamped(
+    const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n, int64_t stamp,
+    uint32_t local_rank, Row* __restrict__ table, uint64_t cap, Misc* __restrict__ misc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    Row row;
+    row.lt = stamp; row.rank = local_rank; row.val = val[i]; row.mod = stamp; row.aux = 0;
+    table[k] = row;
+}
+
+__global__ __launch_bounds__(256) void k_read_rows(
+    const uint32_t* __restrict__ key, uint64_t n, const Row* __restrict__ table, uint64_t cap,
+    int64_t* __restrict__ lt, uint32_t* __restrict__ rank, uint32_t* __restrict__ val,
+    int64_t* __restrict__ mod, Misc* __restrict__ misc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    const Row row = table[k];
+    if (lt) lt[i] = row.lt;
+    if (rank) rank[i] = row.rank;
+    if (val) val[i] = row.val;
+    if (mod) mod[i] = row.mod;
+}
+
+// refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
+__global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, uint64_t n,
+                                                 unsigned long long* __restrict__ out)
+{
+    __shared__ int64_t s[4];
+    int64_t m = INT64_MIN;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const Row row = table[i];
+        if (row.mod >= 0) m = imax(m, row.lt);
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = imax(imax(s[0], s[1]), imax(s[2], s[3]));
+        if (m != INT64_MIN) atomicMax(out, enc(m));
+    }
+}
+
+// recordMap(modifiedSince) (map_crdt.dart:42-45): order-preserving compaction.
+constexpr int kMsPerBlock = 1024;
+__global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table, uint64_t n, int64_t since,
+                                                  uint32_t* __restrict__ counts)
+{
+    __shared__ int s[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kMsPerBlock;
+    int c = 0;
+    for (int q = 0; q < kMsPerBlock / 256; ++q) {
+        const uint64_t i = base + q * 256 + threadIdx.x;
+        if (i < n) c += !(table[i].mod < since);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ __launch_bounds__(1024) void k_ms_scan(uint32_t* __restrict__ counts, uint32_t nb,
+                                                  unsigned long long* __restrict__ total)
+{
+    __shared__ unsigned long long s_wave[16];
+    __shared__ unsigned long long s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t i = base + tid;
+        unsigned long long v = i < nb ? counts[i] : 0;
+        unsigned long long x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            unsigned long long u = __shfl_up(x, off, 64);
+            if (lane >= off) x += u;
+        }
+        if (lane == 63) s_wave[w] = x;
+        __syncthreads();
+        if (w == 0) {
+            unsigned long long y = lane < 16 ? s_wave[lane] : 0;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                unsigned long long u = __shfl_up(y, off, 64);
+                if (lane >= off) y += u;
+            }
+            if (lane < 16) s_wave[lane] = y;
+        }
+        __syncthreads();
+        const unsigned long long pre = (w > 0 ? s_wave[w - 1] : 0) + s_carry;
+        if (i < nb) counts[i] = (uint32_t)(pre + x - v);
+        __syncthreads();
+        if (tid == 0) s_carry += s_wave[15];
+        __syncthreads();
+    }
+    if (tid == 0) *total = s_carry;
+}
+
+__global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table, uint64_t n, int64_t since,
+                                                  const uint32_t* __restrict__ offsets,
+                                                  uint32_t* __restrict__ out)
+{
+    __shared__ int s_wave[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kMsPerBlock;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t run = offsets[blockIdx.x];
+    for (int q = 0; q < kMsPerBlock / 256; ++q) {
+        const uint64_t i = base + q * 256 + threadIdx.x;
+        const bool keep = i < n && !(table[i].mod < since);
+        const unsigned long long b = __ballot(keep);
+        const int before = __popcll(b & ((1ull << lane) - 1));
+        if (lane == 0) s_wave[w] = __popcll(b);
+        __syncthreads();
+        int wpre = 0;
+        for (int k = 0; k < w; ++k) wpre += s_wave[k];
+        const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        if (keep) out[run + wpre + before] = (uint32_t)i;
+        run += tot;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_remap(Row* __restrict__ table, uint64_t n,
+                                               const uint32_t* __restrict__ lut, uint32_t nl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = table[i].rank;
+    if (r < nl) table[i].rank = lut[r];
+}
+
+// ============================================================ host-side context
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; n = 0; }
+        size_t m = std::max<size_t>(want, 16);
+        hipError_t e = hipMalloc(&p, m * sizeof(T));
+        if (e == hipSuccess) n = m;
+        return e;
+    }
+    void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+};
+
+template <typename T>
+struct HBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) { hipHostFree(p); p = nullptr; n = 0; }
+        size_t m = std::max<size_t>(want, 16);
+        hipError_t e = hipHostMalloc(&p, m * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = m;
+        return e;
+    }
+    void release() { if (p) hipHostFree(p); p = nullptr; n = 0; }
+};
+
+}  // namespace
+
+struct crdt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t local_rank = 0;
+    Row* table = nullptr;
+    uint64_t cap = 0;
+    int64_t canonical = 0;
+
+    Misc* d_misc = nullptr;
+    Misc* h_misc = nullptr;            // pinned
+    DBuf<unsigned long long> d_M;      // [R]   (single-ctx merge)
+    DBuf<unsigned long long> d_event;  // [4]
+    DBuf<uint64_t> d_offs;
+    DBuf<uint32_t> d_tstart;
+    HBuf<uint64_t> h_offs;
+    HBuf<uint32_t> h_tstart;
+    DBuf<int64_t> d_T, d_Cprev, d_Rj, d_Cj, d_candP, d_candms;
+    DBuf<uint32_t> d_candtile, d_candkind;
+    DBuf<unsigned long long> d_candkey;
+    // staging of host-memory batches
+    DBuf<uint32_t> s_key, s_rank, s_val;
+    DBuf<int64_t> s_lt, s_millis, s_mod;
+    DBuf<uint8_t> s_flags;
+    DBuf<uint32_t> s_out;
+    DBuf<unsigned long long> d_word;
+    // per-call plan (set by scan, used by later phases)
+    uint32_t plan_R = 0;
+    uint64_t plan_tiles = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> events;
+    std::vector<uint32_t> launched;
+    crdt_timing last_timing{};
+};
+
+namespace {
+
+#define HIPCHK(expr)                                   \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return CRDT_E_HIP;       \
+    } while (0)
+
+#define HIPALLOC(expr)                                                     \
+    do {                                                                   \
+        hipError_t _e = (expr);                                            \
+        if (_e == hipErrorOutOfMemory) return CRDT_E_NOMEM;                \
+        if (_e != hipSuccess) return CRDT_E_HIP;                           \
+    } while (0)
+
+inline unsigned grid_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+
+hipError_t ensure_events(crdt_ctx* c, size_t n) {
+    while (c->events.size() < n) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        c->events.push_back(e);
+    }
+    return hipSuccess;
+}
+
+// Stage a host-memory column into ctx device memory; device-memory columns pass through.
+template <typename T>
+int stage(crdt_ctx* c, DBuf<T>& buf, const T* src, uint64_t n, int32_t mem, const T** out) {
+    if (!src) { *out = nullptr; return CRDT_OK; }
+    if (mem == CRDT_MEM_DEVICE) { *out = src; return CRDT_OK; }
+    HIPALLOC(buf.ensure(n ? n : 1));
+    if (n) HIPCHK(hipMemcpyAsync(buf.p, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *out = buf.p;
+    return CRDT_OK;
+}
+
+struct Cols {
+    const uint32_t* key = nullptr;
+    const int64_t* lt = nullptr;
+    const uint32_t* rank = nullptr;
+    const uint32_t* val = nullptr;
+    const int64_t* millis = nullptr;
+};
+
+int validate_batch(const crdt_batch* b) {
+    if (!b || !b->offsets) return CRDT_E_INVALID;
+    if (b->mem != CRDT_MEM_HOST && b->mem != CRDT_MEM_DEVICE) return CRDT_E_INVALID;
+    if (b->offsets[0] != 0) return CRDT_E_INVALID;
+    for (uint32_t j = 0; j < b->n_changesets; ++j)
+        if (b->offsets[j + 1] < b->offsets[j]) return CRDT_E_INVALID;
+    const uint64_t n = b->offsets[b->n_changesets];
+    if (n > 0 && (!b->lt || !b->rank)) return CRDT_E_INVALID;
+    if ((uint64_t)b->n_changesets >= (1ull << 24)) return CRDT_E_INVALID;
+    for (uint32_t j = 0; j < b->n_changesets; ++j)
+        if (b->offsets[j + 1] - b->offsets[j] >= kLowMask) return CRDT_E_INVALID;
+    return CRDT_OK;
+}
+
+int stage_check_cols(crdt_ctx* c, const crdt_batch* b, Cols* cols) {
+    const uint64_t n = b->offsets[b->n_changesets];
+    int st;
+    if ((st = stage(c, c->s_lt, b->lt, n, b->mem, &cols->lt))) return st;
+    if ((st = stage(c, c->s_rank, b->rank, n, b->mem, &cols->rank))) return st;
+    if ((st = stage(c, c->s_millis, b->millis, n, b->mem, &cols->millis))) return st;
+    return CRDT_OK;
+}
+
+int stage_apply_cols(crdt_ctx* c, const crdt_batch* b, Cols* cols) {
+    const uint64_t n = b->offsets[b->n_changesets];
+    if (n > 0 && (!b->key_id || !b->val)) return CRDT_E_INVALID;
+    int st;
+    if ((st = stage(c, c->s_key, b->key_id, n, b->mem, &cols->key))) return st;
+    if ((st = stage(c, c->s_lt, b->lt, n, b->mem, &cols->lt))) return st;
+    if ((st = stage(c, c->s_rank, b->rank, n, b->mem, &cols->rank))) return st;
+    if ((st = stage(c, c->s_val, b->val, n, b->mem, &cols->val))) return st;
+    return CRDT_OK;
+}
+
+// Upload offsets + per-changeset tile starts; returns total tiles and max tiles.
+int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t* max_tiles) {
+    const uint32_t R = b->n_changesets;
+    HIPALLOC(c->h_offs.ensure(R + 1));
+    HIPALLOC(c->h_tstart.ensure(R + 1));
+    HIPALLOC(c->d_offs.ensure(R + 1));
+    HIPALLOC(c->d_tstart.ensure(R + 1));
+    uint64_t tiles = 0;
+    uint32_t mt = 0;
+    for (uint32_t j = 0; j <= R; ++j) {
+        c->h_offs.p[j] = b->offsets[j];
+        c->h_tstart.p[j] = (uint32_t)tiles;
+        if (j < R) {
+            const uint64_t nj = b->offsets[j + 1] - b->offsets[j];
+            const uint64_t tj = (nj + kTile - 1) / kTile;
+            tiles += tj;
+            mt = std::max<uint32_t>(mt, (uint32_t)tj);
+        }
+    }
+    if (tiles >= (1ull << 32)) return CRDT_E_INVALID;
+    HIPCHK(hipMemcpyAsync(c->d_offs.p, c->h_offs.p, (R + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_tstart.p, c->h_tstart.p, (R + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    *tiles_out = tiles;
+    *max_tiles = mt;
+    return CRDT_OK;
+}
+
+int reset_misc(crdt_ctx* c) {
+    HIPCHK(hipMemsetAsync(c->d_misc, 0, sizeof(Misc), c->stream));
+    return CRDT_OK;
+}
+
+inline void ev_record(crdt_ctx* c, size_t idx) {
+    if (c->timing && idx < c->events.size()) hipEventRecord(c->events[idx], c->stream);
+}
+
+// ---- phases ---------------------------------------------------------------
+int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, unsigned long long* d_maxima) {
+    int st = validate_batch(home);
+    if (st) return st;
+    const uint32_t R = home->n_changesets;
+    Cols cols;
+    if ((st = stage_check_cols(c, home, &cols))) return st;
+    uint64_t tiles = 0;
+    uint32_t mt = 0;
+    if ((st = upload_plan(c, home, &tiles, &mt))) return st;
+    HIPALLOC(c->d_T.ensure(tiles + 1));
+    HIPALLOC(c->d_candtile.ensure(tiles + 1));
+    HIPALLOC(c->d_candkey.ensure(tiles + 1));
+    HIPALLOC(c->d_candP.ensure(tiles + 1));
+    HIPALLOC(c->d_candkind.ensure(tiles + 1));
+    HIPALLOC(c->d_candms.ensure(tiles + 1));
+    if ((st = reset_misc(c))) return st;
+    HIPCHK(hipMemsetAsync(d_maxima, 0, std::max<uint32_t>(R, 1) * sizeof(unsigned long long), c->stream));
+    c->plan_R = R;
+    c->plan_tiles = tiles;
+    if (tiles) {
+        // grid.x: tiles of one changeset strided over at most ~64K blocks in total
+        const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
+        const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
+        for (uint32_t jb = 0; jb < R; jb += 65535) {
+            const uint32_t gy = std::min<uint32_t>(65535, R - jb);
+            k_scan<<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                cols.lt, cols.rank, cols.millis, c->d_offs.p, c->d_tstart.p, jb, c->canonical, wall,
+                c->local_rank, d_maxima, c->d_T.p, c->d_misc, c->d_candtile.p);
+        }
+        HIPCHK(hipGetLastError());
+    }
+    return CRDT_OK;
+}
+
+int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const unsigned long long* d_maxima,
+                unsigned long long* d_event) {
+    const uint32_t R = c->plan_R;
+    if (!home || home->n_changesets != R) return CRDT_E_INVALID;
+    int st;
+    Cols cols;
+    if ((st = stage_check_cols(c, home, &cols))) return st;   // no-op for device batches
+    HIPALLOC(c->d_Cprev.ensure(R + 1));
+    HIPALLOC(c->d_Rj.ensure(R + 1));
+    HIPALLOC(c->d_Cj.ensure(R + 1));
+    HIPCHK(hipMemsetAsync(d_event, 0xFF, 4 * sizeof(unsigned long long), c->stream));
+    if (R) k_clock<<<1, 1024, 0, c->stream>>>(d_maxima, R, wall, c->canonical, c->d_Cprev.p, c->d_Rj.p,
+                                              c->d_Cj.p, d_event);
+    if (c->plan_tiles)
+        k_verify<<<kVerifyBlocks, 64, 0, c->stream>>>(
+            cols.lt, cols.rank, cols.millis, c->d_offs.p, c->d_tstart.p, R, c->d_T.p, c->d_Cprev.p, wall,
+            c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
+            c->d_candms.p, d_event);
+    HIPCHK(hipGetLastError());
+    return CRDT_OK;
+}
+
+int phase_resolve(crdt_ctx* c, unsigned long long* d_event) {
+    k_resolve_local<<<1, 256, 0, c->stream>>>(c->d_misc, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
+                                              c->d_candms.p, d_event);
+    HIPCHK(hipGetLastError());
+    return CRDT_OK;
+}
+
+int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const unsigned long long* d_event,
+                uint8_t* win_flags, crdt_result* out, size_t ev_base) {
+    int st = validate_batch(owned);
+    if (st) return st;
+    const uint32_t R = c->plan_R;
+    if (owned->n_changesets != R) return CRDT_E_INVALID;
+    Cols cols;
+    if ((st = stage_apply_cols(c, owned, &cols))) return st;
+    const uint64_t n = owned->offsets[R];
+    uint8_t* dflags = nullptr;
+    if (win_flags) {
+        if (owned->mem == CRDT_MEM_DEVICE) {
+            dflags = win_flags;
+        } else {
+            HIPALLOC(c->s_flags.ensure(n ? n : 1));
+            dflags = c->s_flags.p;
+        }
+        if (n) HIPCHK(hipMemsetAsync(dflags, 0, n, c->stream));
+    }
+    k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    ev_record(c, ev_base);
+    c->launched.clear();
+    for (uint32_t j = 0; j < R; ++j) {
+        const uint64_t b = owned->offsets[j], e = owned->offsets[j + 1];
+        if (e == b) continue;
+        c->launched.push_back(j);
+        if (c->timing) ev_record(c, ev_base + 1 + 2 * (size_t)j);
+        k_apply<<<grid_for(e - b, kApplyPerBlock), kApplyThreads, 0, c->stream>>>(
+            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        if (c->timing) ev_record(c, ev_base + 2 + 2 * (size_t)j);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    if (win_flags && owned->mem == CRDT_MEM_HOST && n)
+        HIPCHK(hipMemcpyAsync(win_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    crdt_result res = c->h_misc->result;
+    uint64_t np = 0, nw = 0;
+    for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
+    res.n_present = np;
+    res.n_won = nw;
+    if (c->h_misc->err) res.status = CRDT_E_KEY_RANGE;
+    c->canonical = res.canonical_lt;
+    if (out) *out = res;
+    return res.status;
+}
+
+void collect_timing(crdt_ctx* c, uint32_t R, bool full) {
+    crdt_timing t{};
+    if (c->timing && full) {
+        float ms = 0;
+        // events: 0 start, 1 after scan, 2 after clock/verify/resolve, 3 = apply base, then pairs
+        if (hipEventElapsedTime(&ms, c->events[0], c->events[1]) == hipSuccess) t.scan_ms = ms;
+        if (hipEventElapsedTime(&ms, c->events[1], c->events[2]) == hipSuccess) t.clock_ms = ms;
+        for (uint32_t j : c->launched) {
+            const size_t a = 4 + 2 * (size_t)j, b = a + 1;
+            float d = 0;
+            if (hipEventElapsedTime(&d, c->events[a], c->events[b]) == hipSuccess) {
+                t.apply_ms += d;
+                t.apply_launches++;
+            }
+        }
+        const size_t last = 3 + 2 * (size_t)R + 1;
+        if (hipEventElapsedTime(&ms, c->events[0], c->events[last]) == hipSuccess) t.total_ms = ms;
+    }
+    c->last_timing = t;
+}
+
+}  // namespace
+
+// ============================================================== C-ABI entry points
+extern "C" {
+
+int crdt_abi_version(void) { return CRDT_ABI_VERSION; }
+
+const char* crdt_status_string(int s) {
+    switch (s) {
+        case CRDT_OK: return "ok";
+        case CRDT_CLOCK_DRIFT: return "clock drift";
+        case CRDT_DUPLICATE_NODE: return "duplicate node";
+        case CRDT_OVERFLOW: return "counter overflow";
+        case CRDT_E_INVALID: return "invalid argument";
+        case CRDT_E_HIP: return "HIP runtime error";
+        case CRDT_E_NOMEM: return "device out of memory";
+        case CRDT_E_KEY_RANGE: return "key id out of range";
+        case CRDT_E_NO_DEVICE: return "no gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+int crdt_device_count(int* out) {
+    if (!out) return CRDT_E_INVALID;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return CRDT_OK;
+}
+
+int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
+    if (!out) return CRDT_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CRDT_E_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CRDT_E_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CRDT_E_NO_DEVICE;
+    HIPCHK(hipSetDevice(device));
+    crdt_ctx* c = new (std::nothrow) crdt_ctx();
+    if (!c) return CRDT_E_NOMEM;
+    c->device = device;
+    c->local_rank = local_rank;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_misc, sizeof(Misc)) != hipSuccess ||
+        hipHostMalloc(&c->h_misc, sizeof(Misc), hipHostMallocDefault) != hipSuccess ||
+        c->d_M.ensure(1024) != hipSuccess || c->d_event.ensure(4) != hipSuccess ||
+        c->d_word.ensure(4) != hipSuccess) {
+        crdt_destroy(c);
+        return CRDT_E_HIP;
+    }
+    int st = crdt_reserve(c, capacity);
+    if (st) { crdt_destroy(c); return st; }
+    *out = c;
+    return CRDT_OK;
+}
+
+void crdt_destroy(crdt_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->table) hipFree(c->table);
+    if (c->d_misc) hipFree(c->d_misc);
+    if (c->h_misc) hipHostFree(c->h_misc);
+    c->d_M.release(); c->d_event.release(); c->d_offs.release(); c->d_tstart.release();
+    c->h_offs.release(); c->h_tstart.release();
+    c->d_T.release(); c->d_Cprev.release(); c->d_Rj.release(); c->d_Cj.release();
+    c->d_candP.release(); c->d_candms.release(); c->d_candtile.release(); c->d_candkind.release();
+    c->d_candkey.release();
+    c->s_key.release(); c->s_rank.release(); c->s_val.release(); c->s_lt.release();
+    c->s_millis.release(); c->s_mod.release(); c->s_flags.release(); c->s_out.release();
+    c->d_word.release();
+    for (hipEvent_t e : c->events) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int crdt_reserve(crdt_ctx* c, uint64_t capacity) {
+    if (!c) return CRDT_E_INVALID;
+    if (capacity <= c->cap && c->table) return CRDT_OK;
+    if (capacity > (1ull << 32)) return CRDT_E_INVALID;   // key ids are uint32
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t newcap = std::max<uint64_t>(capacity, 16);
+    Row* t = nullptr;
+    HIPALLOC(hipMalloc(&t, newcap * sizeof(Row)));
+    if (c->table && c->cap)
+        HIPCHK(hipMemcpyAsync(t, c->table, c->cap * sizeof(Row), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(t + c->cap, 0x80, (newcap - c->cap) * sizeof(Row), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->table) hipFree(c->table);
+    c->table = t;
+    c->cap = newcap;
+    return CRDT_OK;
+}
+
+int crdt_capacity(const crdt_ctx* c, uint64_t* out) {
+    if (!c || !out) return CRDT_E_INVALID;
+    *out = c->cap;
+    return CRDT_OK;
+}
+
+int crdt_set_local_rank(crdt_ctx* c, uint32_t rank) {
+    if (!c) return CRDT_E_INVALID;
+    c->local_rank = rank;
+    return CRDT_OK;
+}
+
+int crdt_get_canonical(const crdt_ctx* c, int64_t* lt) {
+    if (!c || !lt) return CRDT_E_INVALID;
+    *lt = c->canonical;
+    return CRDT_OK;
+}
+
+int crdt_set_canonical(crdt_ctx* c, int64_t lt) {
+    if (!c) return CRDT_E_INVALID;
+    c->canonical = lt;
+    return CRDT_OK;
+}
+
+int crdt_put_rows(crdt_ctx* c, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
+                  const uint32_t* val, const int64_t* mod, uint64_t n, int32_t mem) {
+    if (!c) return CRDT_E_INVALID;
+    if (n == 0) return CRDT_OK;
+    if (!key_id || !lt || !rank || !val || !mod) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t *dk, *dr, *dv;
+    const int64_t *dl, *dm;
+    int st;
+    if ((st = stage(c, c->s_key, key_id, n, mem, &dk))) return st;
+    if ((st = stage(c, c->s_lt, lt, n, mem, &dl))) return st;
+    if ((st = stage(c, c->s_rank, rank, n, mem, &dr))) return st;
+    if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
+    if ((st = stage(c, c->s_mod, mod, n, mem, &dm))) return st;
+    if ((st = reset_misc(c))) return st;
+    k_put_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dl, dr, dv, dm, n, c->table, c->cap, c->d_misc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return c->h_misc->err ? CRDT_E_KEY_RANGE : CRDT_OK;
+}
+
+int crdt_put_stamped(crdt_ctx* c, const uint32_t* key_id, const uint32_t* val, uint64_t n, int64_t wall,
+                     int32_t mem, crdt_result* out) {
+    if (!c) return CRDT_E_INVALID;
+    crdt_result res;
+    memset(&res, 0, sizeof(res));
+    res.exc_index = UINT64_MAX;
+    res.canonical_lt = c->canonical;
+    if (n == 0) { if (out) *out = res; return CRDT_OK; }     // crdt.dart:48
+    if (!key_id || !val) return CRDT_E_INVALID;
+    // Hlc.send (hlc.dart:51-74), once for the whole call (crdt.dart:40, 50)
+    const int64_t cm = c->canonical >> kShift, cc = c->canonical & kMaxCounter;
+    const int64_t mn = imax(cm, wall);
+    const int64_t cn = (cm == mn) ? cc + 1 : 0;
+    if (wsub(mn, wall) > kMaxDrift) {
+        res.status = CRDT_CLOCK_DRIFT;
+        res.drift_ms = wsub(mn, wall);
+        if (out) *out = res;
+        return res.status;
+    }
+    if (cn > kMaxCounter) {
+        res.status = CRDT_OVERFLOW;
+        res.counter = cn;
+        if (out) *out = res;
+        return res.status;
+    }
+    const int64_t stamp = (int64_t)(((uint64_t)mn << kShift) + (uint64_t)cn);
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t *dk, *dv;
+    int st;
+    if ((st = stage(c, c->s_key, key_id, n, mem, &dk))) return st;
+    if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
+    if ((st = reset_misc(c))) return st;
+    k_put_stamped<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dv, n, stamp, c->local_rank, c->table, c->cap,
+                                                           c->d_misc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_misc->err) return CRDT_E_KEY_RANGE;
+    c->canonical = stamp;
+    res.canonical_lt = stamp;
+    res.n_won = n;
+    if (out) *out = res;
+    return CRDT_OK;
+}
+
+int crdt_read_rows(crdt_ctx* c, const uint32_t* key_id, uint64_t n, int64_t* lt, uint32_t* rank,
+                   uint32_t* val, int64_t* mod, int32_t mem) {
+    if (!c) return CRDT_E_INVALID;
+    if (n == 0) return CRDT_OK;
+    if (!key_id) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t* dk;
+    int st;
+    if ((st = stage(c, c->s_key, key_id, n, mem, &dk))) return st;
+    int64_t *dl = lt, *dm = mod;
+    uint32_t *dr = rank, *dv = val;
+    if (mem == CRDT_MEM_HOST) {
+        HIPALLOC(c->s_lt.ensure(n));
+        HIPALLOC(c->s_mod.ensure(n));
+        HIPALLOC(c->s_rank.ensure(n));
+        HIPALLOC(c->s_val.ensure(n));
+        dl = lt ? c->s_lt.p : nullptr;
+        dm = mod ? c->s_mod.p : nullptr;
+        dr = rank ? c->s_rank.p : nullptr;
+        dv = val ? c->s_val.p : nullptr;
+    }
+    if ((st = reset_misc(c))) return st;
+    k_read_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, n, c->table, c->cap, dl, dr, dv, dm, c->d_misc);
+    HIPCHK(hipGetLastError());
+    if (mem == CRDT_MEM_HOST) {
+        if (lt) HIPCHK(hipMemcpyAsync(lt, dl, n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+        if (mod) HIPCHK(hipMemcpyAsync(mod, dm, n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+        if (rank) HIPCHK(hipMemcpyAsync(rank, dr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        if (val) HIPCHK(hipMemcpyAsync(val, dv, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return c->h_misc->err ? CRDT_E_KEY_RANGE : CRDT_OK;
+}
+
+int crdt_refresh_canonical(crdt_ctx* c, uint64_t n_rows, int64_t* out_lt) {
+    if (!c || n_rows > c->cap) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->d_word.p, 0, sizeof(unsigned long long), c->stream));
+    if (n_rows) {
+        const unsigned g = std::min<unsigned>(grid_for(n_rows, 256), 2048);
+        k_refresh<<<g, 256, 0, c->stream>>>(c->table, n_rows, c->d_word.p);
+        HIPCHK(hipGetLastError());
+    }
+    unsigned long long w = 0;
+    HIPCHK(hipMemcpyAsync(&w, c->d_word.p, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int64_t lt = (w == 0) ? 0 : dec(w);         // empty recordMap -> 0 (crdt.dart:118)
+    c->canonical = lt;                                 // fromLogicalTime(max, nodeId)
+    if (out_lt) *out_lt = lt;
+    return CRDT_OK;
+}
+
+int crdt_modified_since(crdt_ctx* c, uint64_t n_rows, int64_t since_lt, uint32_t* out_ids, uint64_t* n_out) {
+    if (!c || !n_out || n_rows > c->cap) return CRDT_E_INVALID;
+    *n_out = 0;
+    if (n_rows == 0) return CRDT_OK;
+    if (!out_ids) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    const unsigned nb = grid_for(n_rows, kMsPerBlock);
+    HIPALLOC(c->s_out.ensure(n_rows + nb));
+    uint32_t* counts = c->s_out.p + n_rows;
+    k_ms_count<<<nb, 256, 0, c->stream>>>(c->table, n_rows, since_lt, counts);
+    k_ms_scan<<<1, 1024, 0, c->stream>>>(counts, nb, c->d_word.p);
+    k_ms_write<<<nb, 256, 0, c->stream>>>(c->table, n_rows, since_lt, counts, c->s_out.p);
+    HIPCHK(hipGetLastError());
+    unsigned long long total = 0;
+    HIPCHK(hipMemcpyAsync(&total, c->d_word.p, sizeof(total), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (total) HIPCHK(hipMemcpy(out_ids, c->s_out.p, total * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *n_out = total;
+    return CRDT_OK;
+}
+
+int crdt_clear_rows(crdt_ctx* c, uint64_t first, uint64_t count) {
+    if (!c || first > c->cap || count > c->cap - first) return CRDT_E_INVALID;
+    if (count == 0) return CRDT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->table + first, 0x80, count * sizeof(Row), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_remap_ranks(crdt_ctx* c, uint64_t n_rows, const uint32_t* old_to_new, uint32_t n_ranks) {
+    if (!c || n_rows > c->cap || (!old_to_new && n_ranks)) return CRDT_E_INVALID;
+    if (n_rows == 0 || n_ranks == 0) return CRDT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t* dl;
+    int st;
+    if ((st = stage(c, c->s_rank, old_to_new, n_ranks, CRDT_MEM_HOST, &dl))) return st;
+    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table, n_rows, dl, n_ranks);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_flags, crdt_result* out) {
+    if (!c) return CRDT_E_INVALID;
+    int st = validate_batch(batch);
+    if (st) return st;
+    const uint32_t R = batch->n_changesets;
+    if (R == 0) {                                            // no merge() call at all
+        crdt_result res;
+        memset(&res, 0, sizeof(res));
+        res.exc_index = UINT64_MAX;
+        res.canonical_lt = c->canonical;
+        if (out) *out = res;
+        return CRDT_OK;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    // Host batches are staged once; every phase then sees device columns.
+    crdt_batch dev = *batch;
+    uint8_t* dflags = win_flags;
+    const uint64_t n = batch->offsets[R];
+    if (batch->mem == CRDT_MEM_HOST) {
+        Cols cols;
+        if ((st = stage_apply_cols(c, batch, &cols))) return st;
+        if ((st = stage(c, c->s_millis, batch->millis, n, batch->mem, &cols.millis))) return st;
+        dev.key_id = cols.key; dev.lt = cols.lt; dev.rank = cols.rank; dev.val = cols.val;
+        dev.millis = cols.millis;
+        dev.mem = CRDT_MEM_DEVICE;
+        if (win_flags) {
+            HIPALLOC(c->s_flags.ensure(n ? n : 1));
+            dflags = c->s_flags.p;
+        }
+    }
+    HIPALLOC(c->d_M.ensure(R));
+    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
+    ev_record(c, 0);
+    if ((st = phase_scan(c, &dev, wall, c->d_M.p))) return st;
+    ev_record(c, 1);
+    if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
+    if ((st = phase_resolve(c, c->d_event.p))) return st;
+    ev_record(c, 2);
+    st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, 3);
+    if (c->timing) {
+        ev_record(c, 3 + 2 * (size_t)R + 1);
+        hipStreamSynchronize(c->stream);
+    }
+    if (st >= 0 && win_flags && batch->mem == CRDT_MEM_HOST && n)
+        HIPCHK(hipMemcpy(win_flags, dflags, n, hipMemcpyDeviceToHost));
+    collect_timing(c, R, true);
+    return st;
+}
+
+int crdt_merge_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, uint64_t* d_maxima) {
+    if (!c || !d_maxima) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    return phase_scan(c, home, wall, reinterpret_cast<unsigned long long*>(d_maxima));
+}
+
+int crdt_merge_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const uint64_t* d_maxima,
+                     uint64_t* d_event) {
+    if (!c || !d_maxima || !d_event) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    return phase_clock(c, home, wall, reinterpret_cast<const unsigned long long*>(d_maxima),
+                       reinterpret_cast<unsigned long long*>(d_event));
+}
+
+int crdt_merge_resolve(crdt_ctx* c, const crdt_batch* home, uint64_t* d_event) {
+    if (!c || !d_event || !home || home->n_changesets != c->plan_R) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    int st = phase_resolve(c, reinterpret_cast<unsigned long long*>(d_event));
+    if (st) return st;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_merge_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const uint64_t* d_event,
+                     uint8_t* win_flags, crdt_result* out) {
+    if (!c || !d_event) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    const bool timing = c->timing;
+    c->timing = false;
+    int st = phase_apply(c, owned, wall, reinterpret_cast<const unsigned long long*>(d_event), win_flags, out, 0);
+    c->timing = timing;
+    return st;
+}
+
+int crdt_set_timing(crdt_ctx* c, int enable) {
+    if (!c) return CRDT_E_INVALID;
+    c->timing = enable != 0;
+    return CRDT_OK;
+}
+
+int crdt_get_timing(const crdt_ctx* c, crdt_timing* out) {
+    if (!c || !out) return CRDT_E_INVALID;
+    *out = c->last_timing;
+    return CRDT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,246 @@
+"""``DeviceTable``: one replica's row table on one MI355X, over the C-ABI.
+
+Columns may be numpy arrays (host memory, staged by the library) or torch
+tensors already resident on the GPU (zero-copy: their device pointers are
+passed straight through, ``CRDT_MEM_DEVICE``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _capi
+from ._capi import CrdtBatch, CrdtResult, CrdtTiming
+
+
+class CrdtNativeError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _capi.status_string(status) if status else "ok"
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+def _is_torch(a) -> bool:
+    return type(a).__module__.startswith("torch")
+
+
+_NP_TYPES = {"u4": np.uint32, "i8": np.int64, "u1": np.uint8}
+
+
+class _Cols:
+    """Normalises a set of columns to one memory kind and keeps them alive."""
+
+    def __init__(self, **cols):
+        self.keep = []
+        self.mem = None
+        self.ptrs = {}
+        for name, (arr, kind) in cols.items():
+            if arr is None:
+                self.ptrs[name] = None
+                continue
+            if _is_torch(arr):
+                if not arr.is_cuda:
+                    arr = arr.numpy()
+                else:
+                    if not arr.is_contiguous():
+                        raise ValueError(f"column {name} must be contiguous")
+                    mem = _capi.CRDT_MEM_DEVICE
+                    self._set_mem(mem)
+                    self.keep.append(arr)
+                    self.ptrs[name] = ctypes.c_void_p(arr.data_ptr())
+                    continue
+            a = np.ascontiguousarray(arr, dtype=_NP_TYPES[kind])
+            self._set_mem(_capi.CRDT_MEM_HOST)
+            self.keep.append(a)
+            self.ptrs[name] = a.ctypes.data_as(ctypes.c_void_p)
+        if self.mem is None:
+            self.mem = _capi.CRDT_MEM_HOST
+
+    def _set_mem(self, mem):
+        if self.mem is None:
+            self.mem = mem
+        elif self.mem != mem:
+            raise ValueError("all columns of one call must live in the same memory (host or device)")
+
+
+class DeviceTable:
+    """Rows ``{lt, rank, val, mod}`` indexed by key id, plus the canonical clock."""
+
+    def __init__(self, device: int = 0, local_rank: int = 0, capacity: int = 1024):
+        self._lib = _capi.load()
+        self._ctx = ctypes.c_void_p()
+        st = self._lib.crdt_create(device, local_rank, max(int(capacity), 16), ctypes.byref(self._ctx))
+        if st != 0:
+            raise CrdtNativeError(st, "crdt_create")
+        self.device = device
+        self._local_rank = local_rank
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._lib.crdt_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int, what: str):
+        if st < 0:
+            raise CrdtNativeError(st, what)
+        return st
+
+    @property
+    def capacity(self) -> int:
+        v = ctypes.c_uint64()
+        self._check(self._lib.crdt_capacity(self._ctx, ctypes.byref(v)), "crdt_capacity")
+        return v.value
+
+    def reserve(self, capacity: int):
+        if capacity > self.capacity:
+            cap = max(int(capacity), 2 * self.capacity)
+            self._check(self._lib.crdt_reserve(self._ctx, cap), "crdt_reserve")
+
+    @property
+    def canonical(self) -> int:
+        v = ctypes.c_int64()
+        self._check(self._lib.crdt_get_canonical(self._ctx, ctypes.byref(v)), "crdt_get_canonical")
+        return v.value
+
+    @canonical.setter
+    def canonical(self, lt: int):
+        self._check(self._lib.crdt_set_canonical(self._ctx, int(lt)), "crdt_set_canonical")
+
+    @property
+    def local_rank(self) -> int:
+        return self._local_rank
+
+    @local_rank.setter
+    def local_rank(self, r: int):
+        self._check(self._lib.crdt_set_local_rank(self._ctx, int(r)), "crdt_set_local_rank")
+        self._local_rank = int(r)
+
+    # ---------------------------------------------------------------------- SPI
+    def put_rows(self, key, lt, rank, val, mod):
+        c = _Cols(key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), mod=(mod, "i8"))
+        n = len(key)
+        p = c.ptrs
+        self._check(self._lib.crdt_put_rows(self._ctx, p["key"], p["lt"], p["rank"], p["val"], p["mod"],
+                                            n, c.mem), "crdt_put_rows")
+
+    def read_rows(self, key):
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        n = len(key)
+        lt = np.empty(n, np.int64)
+        rank = np.empty(n, np.uint32)
+        val = np.empty(n, np.uint32)
+        mod = np.empty(n, np.int64)
+        if n:
+            P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+            self._check(self._lib.crdt_read_rows(self._ctx, P(key), n, P(lt), P(rank), P(val), P(mod),
+                                                 _capi.CRDT_MEM_HOST), "crdt_read_rows")
+        return lt, rank, val, mod
+
+    def modified_since(self, n_rows: int, since: int) -> np.ndarray:
+        out = np.empty(max(n_rows, 1), np.uint32)
+        n = ctypes.c_uint64()
+        self._check(self._lib.crdt_modified_since(self._ctx, n_rows, int(since),
+                                                  out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n)),
+                    "crdt_modified_since")
+        return out[:n.value]
+
+    def clear_rows(self, first: int, count: int):
+        self._check(self._lib.crdt_clear_rows(self._ctx, first, count), "crdt_clear_rows")
+
+    def remap_ranks(self, n_rows: int, old_to_new):
+        lut = np.ascontiguousarray(old_to_new, dtype=np.uint32)
+        self._check(self._lib.crdt_remap_ranks(self._ctx, n_rows, lut.ctypes.data_as(ctypes.c_void_p),
+                                               len(lut)), "crdt_remap_ranks")
+
+    def refresh_canonical(self, n_rows: int) -> int:
+        v = ctypes.c_int64()
+        self._check(self._lib.crdt_refresh_canonical(self._ctx, n_rows, ctypes.byref(v)),
+                    "crdt_refresh_canonical")
+        return v.value
+
+    # ---------------------------------------------------------------- Crdt API
+    def put_stamped(self, key, val, wall: int) -> dict:
+        c = _Cols(key=(key, "u4"), val=(val, "u4"))
+        res = CrdtResult()
+        self._check(self._lib.crdt_put_stamped(self._ctx, c.ptrs["key"], c.ptrs["val"], len(key), int(wall),
+                                               c.mem, ctypes.byref(res)), "crdt_put_stamped")
+        return res.as_dict()
+
+    def _batch(self, key, lt, rank, val, offsets, millis):
+        c = _Cols(key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), millis=(millis, "i8"))
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        c.keep.append(offs)
+        b = CrdtBatch(c.ptrs["key"], c.ptrs["lt"], c.ptrs["rank"], c.ptrs["val"], c.ptrs["millis"],
+                      offs.ctypes.data_as(ctypes.c_void_p), len(offs) - 1, c.mem)
+        return b, c, offs
+
+    def merge(self, key, lt, rank, val, offsets, wall: int, millis=None, win_flags=True):
+        """R sequential merges (one per changeset); returns (result dict, win flags or None).
+
+        ``win_flags``: True -> a host uint8 array is returned; a torch uint8 CUDA tensor
+        -> filled in place (device batches); False/None -> not produced."""
+        b, c, offs = self._batch(key, lt, rank, val, offsets, millis)
+        n = int(offs[-1])
+        flags_arr = None
+        fptr = None
+        if win_flags is True:
+            if c.mem == _capi.CRDT_MEM_DEVICE:
+                import torch
+                flags_arr = torch.zeros(max(n, 1), dtype=torch.uint8, device=c.keep[0].device)
+                fptr = ctypes.c_void_p(flags_arr.data_ptr())
+            else:
+                flags_arr = np.zeros(max(n, 1), np.uint8)
+                fptr = flags_arr.ctypes.data_as(ctypes.c_void_p)
+        elif win_flags is not None and win_flags is not False:
+            flags_arr = win_flags
+            fptr = ctypes.c_void_p(win_flags.data_ptr()) if _is_torch(win_flags) else \
+                win_flags.ctypes.data_as(ctypes.c_void_p)
+        res = CrdtResult()
+        self._check(self._lib.crdt_merge(self._ctx, ctypes.byref(b), int(wall), fptr, ctypes.byref(res)),
+                    "crdt_merge")
+        if flags_arr is not None and win_flags is True:
+            flags_arr = flags_arr[:n]
+        return res.as_dict(), flags_arr
+
+    # ----------------------------------------------- key-sharded phases (RCCL)
+    def merge_scan(self, home, wall: int, d_maxima):
+        b, c, _ = self._batch(*home)
+        self._check(self._lib.crdt_merge_scan(self._ctx, ctypes.byref(b), int(wall),
+                                              ctypes.c_void_p(d_maxima.data_ptr())), "crdt_merge_scan")
+
+    def merge_clock(self, home, wall: int, d_maxima, d_event):
+        b, c, _ = self._batch(*home)
+        self._check(self._lib.crdt_merge_clock(self._ctx, ctypes.byref(b), int(wall),
+                                               ctypes.c_void_p(d_maxima.data_ptr()),
+                                               ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_clock")
+
+    def merge_resolve(self, home, d_event):
+        b, c, _ = self._batch(*home)
+        self._check(self._lib.crdt_merge_resolve(self._ctx, ctypes.byref(b),
+                                                 ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_resolve")
+
+    def merge_apply(self, owned, wall: int, d_event, win_flags=None):
+        b, c, _ = self._batch(*owned)
+        fptr = None if win_flags is None else ctypes.c_void_p(win_flags.data_ptr())
+        res = CrdtResult()
+        self._check(self._lib.crdt_merge_apply(self._ctx, ctypes.byref(b), int(wall),
+                                               ctypes.c_void_p(d_event.data_ptr()), fptr, ctypes.byref(res)),
+                    "crdt_merge_apply")
+        return res.as_dict()
+
+    # ---------------------------------------------------------------- timing
+    def set_timing(self, enable: bool):
+        self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")
+
+    def timing(self) -> dict:
+        t = CrdtTiming()
+        self._check(self._lib.crdt_get_timing(self._ctx, ctypes.byref(t)), "crdt_get_timing")
+        return t.as_dict()

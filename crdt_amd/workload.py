@@ -1,0 +1,154 @@
+"""Synthetic columnar workloads for the BASELINE.json configurations.
+
+Generated directly in HBM with torch (plumbing only: the merge itself never
+touches torch).  Deterministic for a seed on a given device type.
+
+fanin (configs[3], the metric's workload): R replicas x n records, keys Zipf(s)
+over K ids, unique inside each replica; a local table pre-populated with the
+first ``n_local`` ids.  Keys are sharded over G ranks by ``key % G`` (slot =
+key // G); changeset j is "homed" on rank ``j % G`` (the rank that runs its
+canonical-clock scan).
+
+cfg2 (configs[1]): one 10M-record changeset against a 10M-key table, ~50%
+overlap (5M existing ids + 5M new ids).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+NULL = 0xFFFFFFFF
+BASE_MILLIS = 1_735_689_600_000          # 2025-01-01T00:00:00Z
+
+
+def _zipf_keys(n: int, rows: int, K: int, s: float, gen: torch.Generator, device) -> torch.Tensor:
+    """[rows, n] int64 keys, strictly increasing along each row (unique per replica).
+
+    Stratified inverse-CDF sampling of a continuous Zipf(s) over [1, K+1), then
+    key'_i = i + cummax(key_i - i) forces strict increase (the dense head of the
+    distribution becomes "every hot key once per replica")."""
+    i = torch.arange(n, device=device, dtype=torch.float64)
+    u = (i.unsqueeze(0) + torch.rand(rows, n, device=device, dtype=torch.float64, generator=gen)) / n
+    a = 1.0 - s
+    if abs(a) < 1e-9:
+        x = torch.exp(u * np.log(K + 1.0))
+    else:
+        x = torch.pow(1.0 + u * ((K + 1.0) ** a - 1.0), 1.0 / a)
+    key = (torch.floor(x) - 1).clamp_(0, K - 1).to(torch.int64)
+    del x, u
+    ii = torch.arange(n, device=device, dtype=torch.int64).unsqueeze(0)
+    y = torch.cummax(key - ii, dim=1).values
+    key = y + ii
+    key = torch.minimum(key, (K - n) + ii)           # leave room at the top: still strictly increasing
+    return key
+
+
+def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_local: int = 1 << 27,
+              s: float = 0.8, seed: int = 0xC0FFEE04, device="cuda", order: str = "shuffled",
+              rank: int = 0, world: int = 1, chunk: int = 64, millis_span: int = 1 << 16,
+              counter_span: int = 16) -> dict:
+    dev = torch.device(device)
+    n = -(-total // R)                                   # records per replica (ceil)
+    wall = BASE_MILLIS + millis_span + 1000
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    own = {"key": [], "lt": [], "rank": [], "val": []}
+    own_counts = np.zeros(R, np.int64)
+    home = {"lt": [], "rank": []}
+    home_counts = np.zeros(R, np.int64)
+    for j0 in range(0, R, chunk):
+        rows = min(chunk, R - j0)
+        key = _zipf_keys(n, rows, K, s, gen, dev)
+        if order == "shuffled":
+            perm = torch.argsort(torch.rand(rows, n, device=dev, generator=gen), dim=1)
+            key = torch.gather(key, 1, perm)
+            del perm
+        ms = BASE_MILLIS + torch.randint(0, millis_span, (rows, n), device=dev, generator=gen)
+        cnt = torch.randint(0, counter_span, (rows, n), device=dev, generator=gen)
+        lt = (ms << 16) + cnt
+        del ms, cnt
+        jj = torch.arange(j0, j0 + rows, device=dev, dtype=torch.int64).unsqueeze(1)
+        rk = (jj + 1).expand(rows, n)                    # replica j has node rank j + 1 (local = 0)
+        val = ((jj << 20) | torch.arange(n, device=dev, dtype=torch.int64).unsqueeze(0)) & 0x7FFFFFFF
+        for r_ in range(rows):
+            j = j0 + r_
+            if world > 1 and j % world == rank:
+                home["lt"].append(lt[r_].clone())
+                home["rank"].append(rk[r_].to(torch.int32))
+                home_counts[j] = n
+            if world == 1:
+                m = slice(None)
+                k_own = key[r_]
+            else:
+                m = (key[r_] % world) == rank
+                k_own = key[r_][m] // world
+            own["key"].append(k_own.to(torch.int32))
+            own["lt"].append(lt[r_][m])
+            own["rank"].append(rk[r_][m].to(torch.int32))
+            own["val"].append(val.expand(rows, n)[r_][m].to(torch.int32))
+            own_counts[j] = own["key"][-1].numel()
+        del key, lt, rk, val
+    cat = lambda xs: torch.cat(xs) if xs else torch.zeros(0, device=dev)  # noqa: E731
+    owned = {k: cat(v) for k, v in own.items()}
+    del own
+    if world == 1:                                       # one rank is home to every changeset
+        homed = {"lt": owned["lt"], "rank": owned["rank"]}
+        home_counts = own_counts
+    else:
+        homed = {k: cat(v) for k, v in home.items()}
+    # ---- local table: ids [0, n_local), owned slots only
+    slots_total = -(-K // world)
+    lids = torch.arange(rank, n_local, world, device=dev, dtype=torch.int64)
+    lgen = torch.Generator(device=dev)
+    lgen.manual_seed(seed ^ 0x5EED)
+    nl = lids.numel()
+    # local rows use the same generator on every rank: draw for all ids then pick this shard
+    l_ms = BASE_MILLIS + torch.randint(0, millis_span, (n_local,), device=dev, generator=lgen)
+    l_cnt = torch.randint(0, counter_span, (n_local,), device=dev, generator=lgen)
+    l_rank = torch.randint(0, R + 1, (n_local,), device=dev, generator=lgen)
+    l_lt_all = (l_ms << 16) + l_cnt
+    c0 = int(l_lt_all.max().item())                    # refreshCanonicalTime() of the full replica
+    local = {"slot": (lids // world).to(torch.int32), "lt": l_lt_all[lids].contiguous(),
+             "rank": l_rank[lids].to(torch.int32), "val": (lids & 0x7FFFFFFF).to(torch.int32),
+             "mod": l_lt_all[lids].contiguous()}
+    del l_ms, l_cnt, l_rank, l_lt_all
+    return {
+        "owned": {k: v.contiguous() for k, v in owned.items()},
+        "owned_offsets": np.concatenate([[0], np.cumsum(own_counts)]).astype(np.uint64),
+        "home": {k: v.contiguous() for k, v in homed.items()},
+        "home_offsets": np.concatenate([[0], np.cumsum(home_counts)]).astype(np.uint64),
+        "local": local, "n_local_rows": nl, "capacity": slots_total, "c0": c0, "wall": wall,
+        "R": R, "n_per_replica": n, "total": n * R, "K": K, "n_local": n_local, "world": world, "rank": rank,
+    }
+
+
+def gen_cfg2(n_local: int = 10_000_000, n_remote: int = 10_000_000, overlap: float = 0.5,
+             seed: int = 0xC0FFEE02, device="cuda", millis_span: int = 1 << 20) -> dict:
+    """configs[1]: one changeset; ~overlap of its keys already exist locally."""
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    n_old = int(n_remote * overlap)
+    n_new = n_remote - n_old
+    old = torch.randperm(n_local, device=dev, generator=gen)[:n_old]
+    new = torch.arange(n_local, n_local + n_new, device=dev)
+    key = torch.cat([old, new])
+    key = key[torch.randperm(n_remote, device=dev, generator=gen)]
+    # new ids must appear in first-seen order (interning): renumber them along the stream
+    is_new = key >= n_local
+    key[is_new] = n_local + torch.arange(int(is_new.sum().item()), device=dev)
+    ms = BASE_MILLIS + torch.randint(0, millis_span, (n_remote,), device=dev, generator=gen)
+    lt = (ms << 16) + torch.randint(0, 16, (n_remote,), device=dev, generator=gen)
+    l_ms = BASE_MILLIS + torch.randint(0, millis_span, (n_local,), device=dev, generator=gen)
+    l_lt = (l_ms << 16) + torch.randint(0, 16, (n_local,), device=dev, generator=gen)
+    owned = {"key": key.to(torch.int32), "lt": lt, "rank": torch.ones(n_remote, device=dev, dtype=torch.int32),
+             "val": torch.arange(1, n_remote + 1, device=dev, dtype=torch.int32)}
+    local = {"slot": torch.arange(n_local, device=dev, dtype=torch.int32), "lt": l_lt,
+             "rank": torch.zeros(n_local, device=dev, dtype=torch.int32),
+             "val": torch.arange(n_local, device=dev, dtype=torch.int32), "mod": l_lt.clone()}
+    offs = np.array([0, n_remote], np.uint64)
+    return {"owned": owned, "owned_offsets": offs, "home": {"lt": lt, "rank": owned["rank"]},
+            "home_offsets": offs, "local": local, "n_local_rows": n_local, "capacity": n_local + n_new,
+            "c0": int(l_lt.max().item()), "wall": BASE_MILLIS + millis_span + 1000, "R": 1,
+            "n_per_replica": n_remote, "total": n_remote, "K": n_local + n_new, "n_local": n_local,
+            "world": 1, "rank": 0}

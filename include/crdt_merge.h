@@ -1,0 +1,179 @@
+/* crdt_merge.h — C-ABI of the MI355X-native MapCrdt merge hot path.
+ *
+ * The reference (Dart package `crdt` v4.0.2, /root/reference) has no FFI: its
+ * boundary is the abstract class Crdt<K,V> (lib/src/crdt.dart:7) and its
+ * storage SPI (lib/src/crdt.dart:140-169), implemented by MapCrdt
+ * (lib/src/map_crdt.dart:9-53).  This header is the C surface a dart:ffi shim
+ * subclassing Crdt would bind (INTEGRATION.md shows that binding); every entry
+ * point names the reference member it replaces.
+ *
+ * Data model.  The host (Dart, or the Python mirror in crdt_amd/) owns keys,
+ * values and node-id strings and interns them:
+ *   key_id  : dense uint32 id, assigned in first-committed order, so id order is
+ *             the LinkedHashMap insertion order (map_crdt.dart:10);
+ *   lt      : int64 Hlc.logicalTime = (millis << 16) + counter (hlc.dart:16);
+ *   rank    : uint32 order-preserving rank of the nodeId under Dart
+ *             String.compareTo (hlc.dart:160), so nodeId equality == rank equality;
+ *   val     : uint32 value handle; CRDT_NULL_VALUE marks a tombstone
+ *             (record.dart:17, isDeleted <=> value == null).
+ * The device keeps one 32-byte row per key id: {lt, rank, val, mod, aux} where
+ * mod is Record.modified.logicalTime.  A row whose mod < 0 is invisible to
+ * merge and to recordMap() (map_crdt.dart:42-45); never-written rows hold a
+ * negative mod.
+ *
+ * Domain: |millis| < 2^47 for every clock and wall value (Dart int wraps past it).
+ * Threading: a ctx is one replica (one GPU); calls on one ctx are synchronous and
+ * must not run concurrently, exactly like the single-isolate reference.
+ */
+#ifndef CRDT_MERGE_H
+#define CRDT_MERGE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRDT_ABI_VERSION 1
+#define CRDT_NULL_VALUE 0xFFFFFFFFu
+
+/* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
+ * host rethrows them with the exact messages of hlc.dart:170,179,188. */
+enum crdt_status {
+    CRDT_OK = 0,
+    CRDT_CLOCK_DRIFT = 1,      /* ClockDriftException(drift_ms)         hlc.dart:164-171 */
+    CRDT_DUPLICATE_NODE = 2,   /* DuplicateNodeException(local nodeId)  hlc.dart:182-189 */
+    CRDT_OVERFLOW = 3,         /* OverflowException(counter)            hlc.dart:173-180 */
+    CRDT_E_INVALID = -1,       /* bad argument (offsets, sizes, null pointers) */
+    CRDT_E_HIP = -2,           /* HIP runtime error */
+    CRDT_E_NOMEM = -3,         /* device allocation failed */
+    CRDT_E_KEY_RANGE = -4,     /* a key_id >= capacity: state after the call is unspecified */
+    CRDT_E_NO_DEVICE = -5      /* no usable gfx950 device */
+};
+
+/* Where the column pointers of a call live. */
+enum crdt_mem { CRDT_MEM_HOST = 0, CRDT_MEM_DEVICE = 1 };
+
+typedef struct crdt_ctx crdt_ctx;
+
+/* R remote changesets, concatenated column-wise.  Changeset j is rows
+ * [offsets[j], offsets[j+1]); it is one Map<K, Record<V>> handed to merge()
+ * (crdt.dart:77), in its iteration order, so its key ids must be distinct. */
+typedef struct crdt_batch {
+    const uint32_t* key_id;    /* [n] */
+    const int64_t* lt;         /* [n] */
+    const uint32_t* rank;      /* [n] */
+    const uint32_t* val;       /* [n] */
+    const int64_t* millis;     /* optional [n]: Hlc.millis where it differs from lt >> 16 (a parsed
+                                  counter > 0xFFFF, hlc.dart:43); NULL means millis = lt >> 16 */
+    const uint64_t* offsets;   /* HOST memory, [n_changesets + 1], offsets[0] == 0 */
+    uint32_t n_changesets;
+    int32_t mem;               /* enum crdt_mem of the five column pointers (and win_flags) */
+} crdt_batch;
+
+/* Outcome of a merge / put call. */
+typedef struct crdt_result {
+    int32_t status;            /* enum crdt_status */
+    uint32_t n_stored;         /* changesets whose winners were stored (putRecords ran) */
+    uint32_t exc_changeset;    /* changeset that raised, when status in 1..3 */
+    uint32_t reserved;
+    uint64_t exc_index;        /* record (in that changeset) whose recv() raised; UINT64_MAX when
+                                  send() raised after storing (crdt.dart:93) */
+    int64_t canonical_lt;      /* Crdt._canonicalTime.logicalTime after the call (crdt.dart:9) */
+    int64_t drift_ms;          /* ClockDriftException.drift (hlc.dart:167) */
+    int64_t counter;           /* OverflowException.counter (hlc.dart:176) */
+    uint64_t n_present;        /* records whose key was present in the local snapshot */
+    uint64_t n_won;            /* records stored (winners) */
+} crdt_result;
+
+/* Device-side kernel timing of the last call, measured with HIP events on the
+ * ctx stream (bench / roofline support; zeros unless enabled). */
+typedef struct crdt_timing {
+    double scan_ms;            /* K3a: per-changeset max + candidate tiles */
+    double clock_ms;           /* K3b/K3c: canonical prefix-max scan, exception resolution */
+    double apply_ms;           /* K2: sum over the apply launches */
+    uint32_t apply_launches;
+    uint32_t reserved;
+    double total_ms;           /* first to last event of the call */
+} crdt_timing;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int crdt_abi_version(void);
+const char* crdt_status_string(int status);
+int crdt_device_count(int* out);
+
+/* MapCrdt(nodeId) (map_crdt.dart:16) + Crdt() -> refreshCanonicalTime() on the
+ * empty map (crdt.dart:31-33): canonical lt = 0.  local_rank is the rank of the
+ * local nodeId.  capacity rows are allocated and marked absent. */
+int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out);
+void crdt_destroy(crdt_ctx* ctx);
+int crdt_reserve(crdt_ctx* ctx, uint64_t capacity);          /* grow; new rows absent */
+int crdt_capacity(const crdt_ctx* ctx, uint64_t* out);
+int crdt_set_local_rank(crdt_ctx* ctx, uint32_t rank);        /* after a rank remap */
+
+/* Crdt._canonicalTime (crdt.dart:9-11). */
+int crdt_get_canonical(const crdt_ctx* ctx, int64_t* lt);
+int crdt_set_canonical(crdt_ctx* ctx, int64_t lt);
+
+/* ---- storage SPI (crdt.dart:140-169) --------------------------------------- */
+/* putRecord / putRecords (map_crdt.dart:27-39) and the seed addAll
+ * (map_crdt.dart:17): store rows verbatim, no clock update. */
+int crdt_put_rows(crdt_ctx* ctx, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
+                  const uint32_t* val, const int64_t* mod, uint64_t n, int32_t mem);
+/* getRecord (map_crdt.dart:24): gather rows; any output pointer may be NULL. */
+int crdt_read_rows(crdt_ctx* ctx, const uint32_t* key_id, uint64_t n, int64_t* lt, uint32_t* rank,
+                   uint32_t* val, int64_t* mod, int32_t mem);
+/* recordMap(modifiedSince) filter (map_crdt.dart:42-45): ids in [0, n_rows) with
+ * mod >= since_lt, ascending (= insertion order).  out_ids (HOST) holds n_rows. */
+int crdt_modified_since(crdt_ctx* ctx, uint64_t n_rows, int64_t since_lt, uint32_t* out_ids,
+                        uint64_t* n_out);
+/* purge() (map_crdt.dart:51-52) and rollback of interned-but-uncommitted ids. */
+int crdt_clear_rows(crdt_ctx* ctx, uint64_t first, uint64_t count);
+/* Re-rank stored node ids after the host inserts a new nodeId between existing
+ * ranks: rank := old_to_new[rank] for rows [0, n_rows). */
+int crdt_remap_ranks(crdt_ctx* ctx, uint64_t n_rows, const uint32_t* old_to_new, uint32_t n_ranks);
+
+/* ---- Crdt API ------------------------------------------------------------ */
+/* put / putAll / delete (crdt.dart:39-58): ONE Hlc.send (hlc.dart:51-74) for the
+ * whole call, then rows {C, local_rank, val, C}; n == 0 is a no-op (crdt.dart:48). */
+int crdt_put_stamped(crdt_ctx* ctx, const uint32_t* key_id, const uint32_t* val, uint64_t n,
+                     int64_t wall_millis, int32_t mem, crdt_result* out);
+
+/* refreshCanonicalTime (crdt.dart:114-121) over rows [0, n_rows). */
+int crdt_refresh_canonical(crdt_ctx* ctx, uint64_t n_rows, int64_t* out_lt);
+
+/* R sequential Crdt.merge(changeset_j) calls (crdt.dart:77-94), wall clock
+ * fixed at wall_millis for every clock read (hlc.dart:53,82).  Stops at the
+ * first exception exactly as the reference: a recv() failure in changeset j
+ * stores nothing of j and leaves canonical = the running max before the failing
+ * record; a send() failure after j leaves j stored and canonical = R_j.
+ * win_flags (optional, [n], same memory kind as the batch): 1 where the record
+ * was stored — the Map the reference's removeWhere leaves behind (crdt.dart:80-85)
+ * and the watch() events (map_crdt.dart:36-38). */
+int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint8_t* win_flags,
+               crdt_result* out);
+
+/* ---- key-sharded multi-GPU phases ------------------------------------------
+ * crdt_merge() == scan -> clock -> resolve -> apply on one ctx.  With keys
+ * sharded over G ranks, each rank scans the changesets it is home to (a batch
+ * with all R changesets, non-home ones empty), and between phases the host
+ * all-reduces the device words (RCCL over xGMI):
+ *   d_maxima [R]  u64 : MAX all-reduce after scan
+ *   d_event  [4]  u64 : MIN all-reduce of d_event[0] after clock, MAX of d_event[1..3]
+ *                       after resolve
+ * then applies the records it owns (any rank: owned batch, same n_changesets). */
+int crdt_merge_scan(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis, uint64_t* d_maxima);
+int crdt_merge_clock(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis,
+                     const uint64_t* d_maxima, uint64_t* d_event);
+int crdt_merge_resolve(crdt_ctx* ctx, const crdt_batch* home, uint64_t* d_event);
+int crdt_merge_apply(crdt_ctx* ctx, const crdt_batch* owned, int64_t wall_millis,
+                     const uint64_t* d_event, uint8_t* win_flags, crdt_result* out);
+
+/* ---- measurement ---------------------------------------------------------- */
+int crdt_set_timing(crdt_ctx* ctx, int enable);
+int crdt_get_timing(const crdt_ctx* ctx, crdt_timing* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDT_MERGE_H */

@@ -1,0 +1,291 @@
+"""The drop-in API on the GPU, written like the reference's own tests
+(test/map_crdt_test.dart, test/crdt_test.dart), plus randomized operation
+sequences checked against the object-level oracle."""
+import json
+
+import numpy as np
+import pytest
+
+from crdt_amd import (ClockDriftException, CrdtJson, DuplicateNodeException, Hlc, MapCrdt,
+                      OverflowException, Record)
+
+pytestmark = pytest.mark.gpu
+
+MILLIS = 1000000000000
+ISO = "2001-09-09T01:46:40.000Z"
+WALL = 1700000000000
+
+
+def hlc_now(node="abc", wall=WALL):
+    return Hlc(wall, 0, node)
+
+
+def crdt(node="abc", seed=None):
+    return MapCrdt(node, seed, clock=lambda: WALL)
+
+
+class TestBasic:                                     # crdt_test.dart:12-93
+    def test_node_id(self, gpu_device):
+        assert crdt().nodeId == "abc"
+
+    def test_empty(self, gpu_device):
+        c = crdt()
+        assert c.isEmpty and c.length == 0 and c.map == {} and c.keys == [] and c.values == []
+
+    def test_one_record(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        assert (c.isEmpty, c.length, c.map, c.keys, c.values) == (False, 1, {"x": 1}, ["x"], [1])
+
+    def test_empty_after_deleted(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.delete("x")
+        assert c.isEmpty and c.length == 0 and c.map == {}
+
+    def test_update_existing(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.put("x", 2)
+        assert c.get("x") == 2
+
+    def test_put_many(self, gpu_device):
+        c = crdt()
+        c.putAll({"x": 2, "y": 3})
+        assert (c.get("x"), c.get("y")) == (2, 3)
+
+    def test_delete_value(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.put("y", 2)
+        c.delete("x")
+        assert c.isDeleted("x") is True and c.isDeleted("y") is False
+        assert c.get("x") is None and c.get("y") == 2
+
+    def test_clear(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.put("y", 2)
+        c.clear()
+        assert c.isDeleted("x") and c.isDeleted("y") and c.get("x") is None
+
+    def test_watch(self, gpu_device):               # crdt_test.dart:98-130
+        c = crdt()
+        w_all, w_y = c.watch(), c.watch(key="y")
+        c.put("x", 1)
+        c.put("y", 2)
+        assert w_all.events == [("x", 1), ("y", 2)] and w_y.events == [("y", 2)]
+
+
+class TestSeed:                                      # map_crdt_test.dart:17-31
+    def test_seed_item(self, gpu_device):
+        c = crdt(seed={"x": Record(hlc_now(), 1, hlc_now())})
+        assert c.get("x") == 1 and c.canonicalTime.logicalTime == 0
+
+    def test_seed_and_put(self, gpu_device):
+        c = crdt(seed={"x": Record(hlc_now(), 1, hlc_now())})
+        c.put("x", 2)
+        assert c.get("x") == 2
+
+
+class TestMerge:                                     # map_crdt_test.dart:33-103
+    def test_merge_older(self, gpu_device):
+        c = crdt()
+        c.put("x", 2)
+        c.merge({"x": Record(Hlc(MILLIS - 1, 0, "xyz"), 1, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_very_old(self, gpu_device):
+        c = crdt()
+        c.put("x", 2)
+        c.merge({"x": Record(Hlc(0, 0, "xyz"), 1, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_newer(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.merge({"x": Record(Hlc(WALL + 1, 0, "xyz"), 2, hlc_now())}, wall=WALL + 1)
+        assert c.get("x") == 2
+
+    def test_disambiguate_using_node_id(self, gpu_device):
+        c = crdt()
+        c.merge({"x": Record(Hlc(MILLIS, 0, "nodeA"), 1, hlc_now())})
+        c.merge({"x": Record(Hlc(MILLIS, 0, "nodeB"), 2, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_same(self, gpu_device):
+        c = crdt()
+        c.put("x", 2)
+        ts = c.getRecord("x").hlc
+        c.merge({"x": Record(ts, 1, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_older_newer_counter(self, gpu_device):
+        c = crdt()
+        c.put("x", 2)
+        c.merge({"x": Record(Hlc(MILLIS - 1, 2, "xyz"), 1, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_same_newer_counter(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.merge({"x": Record(Hlc(c.getRecord("x").hlc.millis, 2, "xyz"), 2, hlc_now())})
+        assert c.get("x") == 2
+
+    def test_merge_new_item(self, gpu_device):
+        c = crdt()
+        m = {"x": Record(Hlc(WALL, 0, "xyz"), 2, hlc_now())}
+        c.merge(m)
+        assert c.recordMap() == m
+
+    def test_merge_deleted_item(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.merge({"x": Record(Hlc(WALL + 1, 0, "xyz"), None, hlc_now())}, wall=WALL + 1)
+        assert c.isDeleted("x") is True
+
+    def test_update_hlc_on_merge(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        c.merge({"y": Record(Hlc(MILLIS - 1, 0, "xyz"), 2, hlc_now())})
+        assert c.values == [1, 2]
+
+    def test_merge_mutates_map_to_winners(self, gpu_device):   # crdt.dart:80-85
+        c = crdt()
+        c.put("x", 5)
+        m = {"x": Record(Hlc(0, 0, "xyz"), 1, hlc_now()), "y": Record(Hlc(1, 0, "xyz"), 2, hlc_now())}
+        c.merge(m)
+        assert list(m) == ["y"]
+
+    def test_duplicate_node_raises_and_leaves_state(self, gpu_device):
+        c = crdt()
+        c.put("x", 1)
+        before = c.canonicalTime
+        m = {"y": Record(Hlc(WALL + 5, 0, "abc"), 2, hlc_now())}
+        with pytest.raises(DuplicateNodeException) as e:
+            c.merge(m)
+        assert str(e.value) == "Duplicate node: abc"
+        assert c.get("y") is None and not c.containsKey("y") and list(m) == ["y"]
+        assert c.canonicalTime == before
+
+    def test_drift_raises(self, gpu_device):
+        c = crdt()
+        with pytest.raises(ClockDriftException) as e:
+            c.merge({"y": Record(Hlc(WALL + 60001, 0, "q"), 2, hlc_now())})
+        assert e.value.drift == 60001
+
+
+class TestSerialization:                             # map_crdt_test.dart:105-201
+    def test_json_encode(self, gpu_device):
+        hlcNow = hlc_now()
+        c = crdt(seed={"x": Record(Hlc(MILLIS, 0, "abc"), 1, hlcNow)})
+        assert c.toJson() == f'{{"x":{{"hlc":"{ISO}-0000-abc","value":1}}}}'
+        c2 = MapCrdt("abc", {1: Record(Hlc(MILLIS, 0, "abc"), 1, hlcNow)})
+        assert c2.toJson() == f'{{"1":{{"hlc":"{ISO}-0000-abc","value":1}}}}'
+
+    def test_json_decode_put_records(self, gpu_device):
+        c = crdt()
+        c.putRecords(CrdtJson.decode(f'{{"x":{{"hlc":"{ISO}-0000-abc","value":1}}}}', hlc_now()))
+        assert c.recordMap() == {"x": Record(Hlc(MILLIS, 0, "abc"), 1, hlc_now())}
+
+    def test_merge_json_example(self, gpu_device):   # example/crdt_example.dart
+        c = crdt("node_id")
+        c.put("a", 1)
+        remote = json.dumps({"a": {"hlc": str(Hlc(WALL + 1, 0, "another_nodeId")), "value": 2}})
+        c.mergeJson(remote, wall=WALL + 1)
+        assert c.get("a") == 2
+
+
+class TestDeltaSync:                                 # map_crdt_test.dart:203-279
+    def test_delta_subsets(self, gpu_device):
+        h1, h2, h3 = Hlc(MILLIS, 0, "abc"), Hlc(MILLIS + 1, 0, "abc"), Hlc(MILLIS + 2, 0, "abc")
+        c = crdt(seed={"x": Record(h1, 1, h1), "y": Record(h2, 2, h2)})
+        assert [len(c.recordMap(modifiedSince=h)) for h in (None, h1, h2, h3)] == [2, 2, 1, 0]
+
+    @staticmethod
+    def _sync(local, remote, wall):
+        time = local.canonicalTime
+        remote.merge(local.recordMap(), wall=wall)
+        local.merge(remote.recordMap(modifiedSince=time), wall=wall)
+
+    def test_in_order_and_reverse(self, gpu_device):
+        for order in ("in", "reverse"):
+            a, b, cc = MapCrdt("a"), MapCrdt("b"), MapCrdt("c")
+            a.put("x", 1, wall=WALL)
+            b.put("x", 2, wall=WALL + 100)
+            if order == "in":
+                self._sync(a, cc, WALL + 200)
+                self._sync(b, cc, WALL + 200)
+                assert (a.get("x"), b.get("x"), cc.get("x")) == (1, 2, 2)
+            else:
+                self._sync(b, cc, WALL + 200)
+                self._sync(a, cc, WALL + 200)
+                self._sync(b, cc, WALL + 200)
+                assert (a.get("x"), b.get("x"), cc.get("x")) == (2, 2, 2)
+
+
+def _random_ops_vs_oracle(seed, n_ops=40):
+    from oracle import crdt_oracle as O
+    rng = np.random.default_rng(seed)
+    nodes = ["local", "a", "m", "zz", "b0", "~"]
+    dev, ora = MapCrdt("local"), O.MapCrdt("local")
+    wall = WALL
+    for _ in range(n_ops):
+        wall += int(rng.integers(0, 3))
+        op = rng.integers(0, 5)
+        try:
+            if op == 0:
+                k, v = f"k{rng.integers(0, 30)}", int(rng.integers(0, 100))
+                e1 = e2 = None
+                try:
+                    dev.put(k, v, wall=wall)
+                except Exception as ex:  # noqa: BLE001
+                    e1 = type(ex).__name__
+                try:
+                    ora.put(k, v, wall)
+                except Exception as ex:  # noqa: BLE001
+                    e2 = type(ex).__name__
+                assert e1 == e2
+            else:
+                R = int(rng.integers(1, 4))
+                css_d, css_o = [], []
+                for _ in range(R):
+                    keys = rng.choice(40, int(rng.integers(0, 15)), replace=False)
+                    cs_d, cs_o = {}, {}
+                    for k in keys:
+                        ms = wall + int(rng.integers(-50, 8)) + (60001 if rng.random() < 0.01 else 0)
+                        node = nodes[int(rng.integers(0, len(nodes)))] if rng.random() < 0.97 else "local"
+                        cnt = int(rng.integers(0, 3))
+                        val = None if rng.random() < 0.15 else int(rng.integers(0, 1000))
+                        cs_d[f"k{k}"] = Record(Hlc(ms, cnt, node), val, Hlc(0, 0, "local"))
+                        cs_o[f"k{k}"] = O.Record(O.Hlc(ms, cnt, node), val, O.Hlc(0, 0, "local"))
+                    css_d.append(cs_d)
+                    css_o.append(cs_o)
+                e1 = e2 = None
+                try:
+                    dev.mergeAll(css_d, wall=wall)
+                except Exception as ex:  # noqa: BLE001
+                    e1 = (type(ex).__name__, str(ex))
+                try:
+                    for cs in css_o:
+                        ora.merge(cs, wall)
+                except Exception as ex:  # noqa: BLE001
+                    e2 = (type(ex).__name__, str(ex))
+                assert e1 == e2
+                for a, b in zip(css_d, css_o):
+                    assert list(a) == list(b)           # same removeWhere mutation
+        finally:
+            pass
+        rm_d, rm_o = dev.recordMap(), ora.record_map()
+        assert list(rm_d) == list(rm_o)                 # same LinkedHashMap order
+        for k in rm_o:
+            assert rm_d[k].hlc.logicalTime == rm_o[k].hlc.logical_time
+            assert rm_d[k].hlc.nodeId == rm_o[k].hlc.node_id
+            assert rm_d[k].value == rm_o[k].value
+            assert rm_d[k].modified.logicalTime == rm_o[k].modified.logical_time
+        assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_operation_sequences(gpu_device, seed):
+    _random_ops_vs_oracle(seed)

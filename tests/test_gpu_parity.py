@@ -1,0 +1,151 @@
+"""GPU parity: the HIP merge path (through the C-ABI) against the golden vectors
+and the C restatement, bit for bit — rows, win flags, canonical, exceptions."""
+import numpy as np
+import pytest
+
+from tests._cases import ABSENT_MOD, CASE_SPECS, NULL, make_case, oracle_run
+from tests.test_golden_cpu import check_rows, golden_case
+
+pytestmark = pytest.mark.gpu
+
+RESULT_FIELDS = ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter",
+                 "n_present", "n_won")
+
+
+def device_run(case, device_cols=False, capacity=None):
+    from crdt_amd import DeviceTable
+    t = DeviceTable(0, local_rank=case["local_rank"], capacity=capacity or case["n_ids"])
+    loc = case["local"]
+    keep = loc["mod"] != ABSENT_MOD
+    ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
+    if len(ids):
+        t.put_rows(ids, loc["lt"][keep], loc["rank"][keep], loc["val"][keep], loc["mod"][keep])
+    t.canonical = case["c0"]
+    cols = [case["key"], case["lt"], case["rank"], case["val"]]
+    millis = case["millis"]
+    if device_cols:
+        import torch
+        cols = [torch.from_numpy(c.astype(c.dtype)).cuda() for c in cols]
+        millis = None if millis is None else torch.from_numpy(millis).cuda()
+    res, flags = t.merge(*cols, case["offsets"], case["wall"], millis=millis)
+    if device_cols:
+        flags = flags.cpu().numpy()
+    lt, rank, val, mod = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
+    assert t.canonical == res["canonical_lt"]
+    t.close()
+    return (lt, rank, val, mod), res, flags
+
+
+@pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
+def test_golden_vectors(gpu_device, name):
+    case, exp, expected = golden_case(name)
+    rows, res, flags = device_run(case)
+    check_rows(*rows, exp)
+    assert np.array_equal(flags, exp["flags"])
+    for k, v in expected.items():
+        assert res[k] == v, (name, k, res[k], v)
+
+
+def compare_with_oracle(case, **kw):
+    rows, res, flags = device_run(case, **kw)
+    orows, ores, oflags = oracle_run(case)
+    for f, a in zip(("lt", "rank", "val", "mod"), rows):
+        assert np.array_equal(a, orows[f]), f
+    assert np.array_equal(flags, oflags)
+    for k in RESULT_FIELDS:
+        assert res[k] == ores[k], (k, res[k], ores[k])
+    return res
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_small(gpu_device, seed):
+    rng = np.random.default_rng(1000 + seed)
+    kw = dict(seed=2000 + seed, R=int(rng.integers(1, 12)), per_cs=int(rng.integers(0, 500)),
+              n_local=int(rng.integers(1, 600)), n_new=int(rng.integers(0, 400)),
+              millis_span=int(rng.integers(1, 100)), counter_span=int(rng.integers(1, 8)),
+              n_ranks=int(rng.integers(2, 40)), tomb_frac=float(rng.random() * 0.5),
+              neg_mod_frac=float(rng.random() * 0.1), dup_frac=float(rng.random() * 0.01),
+              drift_frac=float(rng.random() * 0.005))
+    kw["local_rank"] = int(rng.integers(0, kw["n_ranks"]))
+    compare_with_oracle(make_case(**kw))
+
+
+def test_device_resident_columns(gpu_device):
+    """Zero-copy path: torch CUDA tensors go straight to the kernels."""
+    compare_with_oracle(make_case(seed=77, R=5, per_cs=3000, n_local=6000, n_new=3000), device_cols=True)
+
+
+def test_large_single_changeset(gpu_device):
+    """One changeset of 1M records: many scan tiles, many apply blocks."""
+    res = compare_with_oracle(make_case(seed=78, R=1, per_cs=1_000_000, n_local=1_200_000, n_new=800_000,
+                                        millis_span=1 << 16))
+    assert res["status"] == 0 and res["n_won"] > 0
+
+
+def test_many_changesets(gpu_device):
+    compare_with_oracle(make_case(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8,
+                                  counter_span=4, n_ranks=301))
+
+
+def test_exception_in_late_tile(gpu_device):
+    """A raising record deep inside a big changeset: candidate tile far from the start."""
+    case = make_case(seed=80, R=2, per_cs=200_000, n_local=300_000, n_new=100_000,
+                     force=[(1, 150_001, "drift")], millis_span=1 << 12)
+    res = compare_with_oracle(case)
+    assert res["status"] == 1 and res["exc_changeset"] == 1 and res["exc_index"] == 150_001
+
+
+def test_false_candidates_do_not_raise(gpu_device):
+    """Flagged records above C0 that are NOT prefix maxima must not raise."""
+    rng = np.random.default_rng(5)
+    case = make_case(seed=81, R=1, per_cs=50_000, n_local=60_000, n_new=0, c0=0, millis_span=1000)
+    # first record is the global max (foreign); later dups exceed C0 but not the running max
+    case["lt"][0] = int(case["lt"].max()) + 10
+    dups = rng.choice(np.arange(1, 50_000), 500, replace=False)
+    case["rank"][dups] = case["local_rank"]
+    res = compare_with_oracle(case)
+    assert res["status"] == 0
+
+
+def test_put_stamped_and_views(gpu_device):
+    from crdt_amd import DeviceTable
+    from oracle.oracle_c import OracleTable
+    from tests._cases import WALL
+    t = DeviceTable(0, local_rank=2, capacity=100)
+    o = OracleTable(100, 2, 0)
+    key = np.array([5, 9, 3], np.uint32)
+    val = np.array([1, NULL, 7], np.uint32)
+    r1 = t.put_stamped(key, val, WALL)
+    r2 = o.put_stamped(key, val, WALL)
+    assert r1["canonical_lt"] == r2.canonical_lt == WALL << 16
+    r1 = t.put_stamped(key[:1], val[:1], WALL)                 # same wall: counter + 1
+    r2 = o.put_stamped(key[:1], val[:1], WALL)
+    assert r1["canonical_lt"] == r2.canonical_lt == (WALL << 16) + 1
+    lt, rank, v, mod = t.read_rows(np.arange(100, dtype=np.uint32))
+    assert np.array_equal(lt, o.rows["lt"]) and np.array_equal(mod, o.rows["mod"])
+    assert t.refresh_canonical(100) == o.refresh(100)
+    assert np.array_equal(t.modified_since(100, (WALL << 16) + 1), o.modified_since(100, (WALL << 16) + 1))
+    assert np.array_equal(t.modified_since(100, 0), np.array([3, 5, 9], np.uint32))
+    t.remap_ranks(100, [0, 1, 4, 5, 6])
+    assert t.read_rows(np.array([5], np.uint32))[1][0] == 4
+    t.clear_rows(0, 100)
+    assert np.all(t.read_rows(np.arange(100, dtype=np.uint32))[3] < 0)
+    assert t.refresh_canonical(100) == 0
+
+
+def test_key_out_of_range_is_reported_not_faulting(gpu_device):
+    from crdt_amd import CrdtNativeError, DeviceTable
+    t = DeviceTable(0, local_rank=0, capacity=64)
+    with pytest.raises(CrdtNativeError):
+        t.merge(np.array([1, 10_000], np.uint32), np.array([5, 6], np.int64), np.array([1, 1], np.uint32),
+                np.array([0, 0], np.uint32), np.array([0, 2], np.uint64), 1 << 40)
+
+
+def test_reserve_preserves_rows(gpu_device):
+    from crdt_amd import DeviceTable
+    t = DeviceTable(0, local_rank=0, capacity=16)
+    t.put_rows(np.array([3], np.uint32), np.array([42], np.int64), np.array([1], np.uint32),
+               np.array([7], np.uint32), np.array([43], np.int64))
+    t.reserve(100_000)
+    lt, rank, val, mod = t.read_rows(np.array([3, 99_999], np.uint32))
+    assert (lt[0], rank[0], val[0], mod[0]) == (42, 1, 7, 43) and mod[1] < 0
