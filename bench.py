@@ -98,21 +98,17 @@ def main():
         table.canonical = wl["c0"]
         torch.cuda.synchronize()
 
+    from crdt_amd.dist import sharded_merge, torch_reducers
+    if world > 1:
+        red_max, red_min = torch_reducers(dist)
+
     def step(flags=None):
         if world == 1:
             res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
             return res
         # key-sharded: home scan -> MAX(M_j) -> clock -> MIN(event) -> resolve -> MAX(details) -> apply
-        table.merge_scan(home_cols, wl["wall"], d_max)
-        dist.all_reduce(d_max.view(torch.uint64) if hasattr(torch, "uint64") else d_max, op=dist.ReduceOp.MAX)
-        table.merge_clock(home_cols, wl["wall"], d_max, d_ev)
-        ev0 = d_ev[:1]
-        dist.all_reduce(ev0.view(torch.uint64) if hasattr(torch, "uint64") else ev0, op=dist.ReduceOp.MIN)
-        table.merge_resolve(home_cols, d_ev)
-        rest = d_ev[1:]
-        dist.all_reduce(rest.view(torch.uint64) if hasattr(torch, "uint64") else rest, op=dist.ReduceOp.MAX)
-        torch.cuda.synchronize()
-        return table.merge_apply(own_cols, wl["wall"], d_ev, win_flags=flags)
+        return sharded_merge(table, home_cols, own_cols, wl["wall"], d_max, d_ev, red_max, red_min,
+                             win_flags=flags)
 
     def barrier():
         if world > 1:
@@ -123,7 +119,7 @@ def main():
         reset()
         step()
     table.set_timing(True)
-    step_ms, apply_ms, apply_launches, scan_ms = [], 0.0, 0, 0.0
+    step_ms, apply_ms, apply_launches, scan_ms, clock_ms, dev_ms = [], 0.0, 0, 0.0, 0.0, 0.0
     res = None
     for _ in range(args.steps):
         reset()
@@ -141,6 +137,8 @@ def main():
         apply_ms += tm["apply_ms"]
         apply_launches += tm["apply_launches"]
         scan_ms += tm["scan_ms"]
+        clock_ms += tm["clock_ms"]
+        dev_ms += tm["total_ms"]
     table.set_timing(False)
     assert res["status"] == 0, res
     ms_per_step = float(np.mean(step_ms))
@@ -196,6 +194,9 @@ def main():
                    "parallelism": f"keyshard{world}" if world > 1 else "single",
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu,
+        "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
+                         "apply_kernels": round(apply_ms / args.steps, 3), "apply_launches": apply_launches // args.steps,
+                         "device_total": round(dev_ms / args.steps, 3)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

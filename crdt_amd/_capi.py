@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcrdt_mi355x.so")
@@ -100,6 +101,14 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same SONAME
+    # libamdhip64.so.7).  Loaded first, it is the one our library binds to; loaded after us
+    # it would bring a second runtime whose device enumeration then fails.
+    if os.environ.get("CRDT_AMD_NO_TORCH") != "1" and "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise NativeLibraryMissing(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"

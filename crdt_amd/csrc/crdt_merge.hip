@@ -43,10 +43,14 @@ constexpr int kApplyPerBlock = kApplyThreads * kApplyItems;
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
 
-constexpr uint64_t kLowBits = 40;
-constexpr uint64_t kLowMask = (1ull << kLowBits) - 1;  // event low word == kLowMask: send() failure
-constexpr uint64_t kEvNone = ~0ull;
-constexpr uint64_t kSign = 1ull << 63;
+// Collective words are plain signed int64 so an RCCL MAX / MIN all-reduce combines them:
+//   maxima[j]  = M_j, INT64_MIN when changeset j is empty (or not homed here)
+//   event[0]   = (j << 40) | i  for a recv() failure at record i of changeset j,
+//                (j << 40) | kLowMask for a send() failure after j;  INT64_MAX: none
+//   event[1..3]= canonical at the failure / kind / Hlc.millis; INT64_MIN, 0, INT64_MIN: none
+constexpr int64_t kLowBits = 40;
+constexpr int64_t kLowMask = (1ll << kLowBits) - 1;
+constexpr int64_t kEvNone = INT64_MAX;
 
 // One device row per key id.  32-byte aligned: a random access is one 32-B sector.
 struct alignas(32) Row {
@@ -69,8 +73,6 @@ struct Misc {
     unsigned long long won[kCounterSlots];
 };
 
-__host__ __device__ inline unsigned long long enc(int64_t x) { return (unsigned long long)x ^ kSign; }
-__host__ __device__ inline int64_t dec(unsigned long long u) { return (int64_t)(u ^ kSign); }
 __host__ __device__ inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
 __host__ __device__ inline int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
 
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
-    int64_t wall, uint32_t local_rank, unsigned long long* __restrict__ M,
+    int64_t wall, uint32_t local_rank, long long* __restrict__ M,
     int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
 {
     __shared__ int64_t s_max[kScanThreads / 64];
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             int tf = s_flag[0];
             for (int k = 1; k < kScanThreads / 64; ++k) { tm = imax(tm, s_max[k]); tf |= s_flag[k]; }
             T[t0 + t] = tm;
-            atomicMax(&M[j], enc(tm));
+            atomicMax(&M[j], (long long)tm);
             if (tf) {
                 const uint32_t c = atomicAdd(&misc->cand_count, 1u);
                 cand_tile[c] = t0 + t;
@@ -158,9 +160,9 @@ __device__ inline bool send_fails(int64_t r, int64_t wall) {
 }
 
 __global__ __launch_bounds__(1024) void k_clock(
-    const unsigned long long* __restrict__ M, uint32_t R, int64_t wall, int64_t c0,
+    const long long* __restrict__ M, uint32_t R, int64_t wall, int64_t c0,
     int64_t* __restrict__ Cprev, int64_t* __restrict__ Rj, int64_t* __restrict__ Cj,
-    unsigned long long* __restrict__ event)
+    long long* __restrict__ event)
 {
     __shared__ int64_t s_wave[16];
     __shared__ uint32_t s_first;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(1024) void k_clock(
         const uint32_t j = base + tid;
         const bool valid = j < R;
         const int64_t jj = (int64_t)j + 1;
-        const int64_t mj = valid ? dec(M[j]) : INT64_MIN;
+        const int64_t mj = valid ? (int64_t)M[j] : INT64_MIN;
         const bool has = mj != INT64_MIN;
         const int64_t b = has ? imax(mj + 1, W) : W;
         const int64_t key = valid ? b - jj : INT64_MIN;
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(1024) void k_clock(
     if (first != UINT32_MAX) atomicMin(&s_first, first);
     __syncthreads();
     if (tid == 0 && s_first != UINT32_MAX)
-        atomicMin(event, ((unsigned long long)s_first << kLowBits) | kLowMask);
+        atomicMin(event, (long long)(((int64_t)s_first << kLowBits) | kLowMask));
 }
 
 // =============================================================================
@@ -227,9 +229,9 @@ __global__ __launch_bounds__(64) void k_verify(
     const uint32_t* __restrict__ tstart, uint32_t R, const int64_t* __restrict__ T,
     const int64_t* __restrict__ Cprev, int64_t wall, uint32_t local_rank,
     const Misc* __restrict__ misc, const uint32_t* __restrict__ cand_tile,
-    unsigned long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
+    long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
     uint32_t* __restrict__ cand_kind, int64_t* __restrict__ cand_ms,
-    unsigned long long* __restrict__ event)
+    long long* __restrict__ event)
 {
     const int lane = threadIdx.x;
     const uint32_t n = misc->cand_count;
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(64) void k_verify(
         }
         if (lane == 0) {
             if (found) {
-                const unsigned long long key = ((unsigned long long)j << kLowBits) | (fi - offs[j]);
+                const long long key = (long long)(((int64_t)j << kLowBits) | (int64_t)(fi - offs[j]));
                 cand_key[c] = key;
                 cand_P[c] = fp;
                 cand_kind[c] = fkind;
@@ -292,22 +294,22 @@ __global__ __launch_bounds__(64) void k_verify(
 }
 
 // Publish the recv-failure details of the global first event if this ctx holds
-// it: event[1] = enc(canonical at failure), event[2] = kind, event[3] = enc(millis).
+// it: event[1] = canonical at the failure, event[2] = kind, event[3] = Hlc.millis.
 __global__ __launch_bounds__(256) void k_resolve_local(
-    const Misc* __restrict__ misc, const unsigned long long* __restrict__ cand_key,
+    const Misc* __restrict__ misc, const long long* __restrict__ cand_key,
     const int64_t* __restrict__ cand_P, const uint32_t* __restrict__ cand_kind,
-    const int64_t* __restrict__ cand_ms, unsigned long long* __restrict__ event)
+    const int64_t* __restrict__ cand_ms, long long* __restrict__ event)
 {
-    const unsigned long long ev = event[0];
-    if (threadIdx.x == 0) { event[1] = 0; event[2] = 0; event[3] = 0; }
+    const long long ev = event[0];
+    if (threadIdx.x == 0) { event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
     __syncthreads();
     if (ev == kEvNone || (ev & kLowMask) == kLowMask) return;
     const uint32_t n = misc->cand_count;
     for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
         if (cand_key[c] == ev) {
-            event[1] = enc(cand_P[c]);
+            event[1] = cand_P[c];
             event[2] = cand_kind[c];
-            event[3] = enc(cand_ms[c]);
+            event[3] = cand_ms[c];
         }
     }
 }
@@ -316,14 +318,14 @@ __global__ __launch_bounds__(256) void k_resolve_local(
 // K3d — k_resolve: stop point, status, final canonical (crdt.dart:80-93 order:
 // every recv of changeset j, then its store, then its send).
 // =============================================================================
-__global__ void k_resolve(const unsigned long long* __restrict__ event, uint32_t R, int64_t wall,
+__global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64_t wall,
                           int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
                           Misc* __restrict__ misc)
 {
     if (threadIdx.x != 0) return;
     crdt_result res = {};
     res.exc_index = UINT64_MAX;
-    const unsigned long long ev = event[0];
+    const int64_t ev = event[0];
     uint32_t stop;
     if (ev == kEvNone) {
         stop = R;
@@ -331,7 +333,7 @@ __global__ void k_resolve(const unsigned long long* __restrict__ event, uint32_t
         res.canonical_lt = R ? Cj[R - 1] : c0;
     } else {
         const uint32_t j = (uint32_t)(ev >> kLowBits);
-        const uint64_t low = ev & kLowMask;
+        const int64_t low = ev & kLowMask;
         res.exc_changeset = j;
         if (low == kLowMask) {                       // send() after storing changeset j
             stop = j + 1;
@@ -348,10 +350,10 @@ __global__ void k_resolve(const unsigned long long* __restrict__ event, uint32_t
             }
         } else {                                     // recv() inside changeset j
             stop = j;
-            res.exc_index = low;
-            res.canonical_lt = dec(event[1]);
+            res.exc_index = (uint64_t)low;
+            res.canonical_lt = event[1];
             res.status = (int32_t)event[2];
-            if (res.status == CRDT_CLOCK_DRIFT) res.drift_ms = wsub(dec(event[3]), wall);
+            if (res.status == CRDT_CLOCK_DRIFT) res.drift_ms = wsub(event[3], wall);
         }
     }
     res.n_stored = stop;
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(256) void k_read_rows(
 
 // refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
 __global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, uint64_t n,
-                                                 unsigned long long* __restrict__ out)
+                                                 long long* __restrict__ out)
 {
     __shared__ int64_t s[4];
     int64_t m = INT64_MIN;
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, 
     __syncthreads();
     if (threadIdx.x == 0) {
         m = imax(imax(s[0], s[1]), imax(s[2], s[3]));
-        if (m != INT64_MIN) atomicMax(out, enc(m));
+        if (m != INT64_MIN) atomicMax(out, (long long)m);
     }
 }
 
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table,
 }
 
 __global__ __launch_bounds__(1024) void k_ms_scan(uint32_t* __restrict__ counts, uint32_t nb,
-                                                  unsigned long long* __restrict__ total)
+                                                  long long* __restrict__ total)
 {
     __shared__ unsigned long long s_wave[16];
     __shared__ unsigned long long s_carry;
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(1024) void k_ms_scan(uint32_t* __restrict__ counts,
         if (tid == 0) s_carry += s_wave[15];
         __syncthreads();
     }
-    if (tid == 0) *total = s_carry;
+    if (tid == 0) *total = (long long)s_carry;
 }
 
 __global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table, uint64_t n, int64_t since,
@@ -578,6 +580,17 @@ __global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table,
         run += tot;
         __syncthreads();
     }
+}
+
+__global__ __launch_bounds__(256) void k_fill_i64(long long* __restrict__ p, uint64_t n, long long v)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__global__ void k_event_init(long long* __restrict__ event)
+{
+    if (threadIdx.x == 0) { event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
 }
 
 __global__ __launch_bounds__(256) void k_remap(Row* __restrict__ table, uint64_t n,
@@ -632,21 +645,21 @@ struct crdt_ctx {
 
     Misc* d_misc = nullptr;
     Misc* h_misc = nullptr;            // pinned
-    DBuf<unsigned long long> d_M;      // [R]   (single-ctx merge)
-    DBuf<unsigned long long> d_event;  // [4]
+    DBuf<long long> d_M;               // [R]   (single-ctx merge)
+    DBuf<long long> d_event;           // [4]
     DBuf<uint64_t> d_offs;
     DBuf<uint32_t> d_tstart;
     HBuf<uint64_t> h_offs;
     HBuf<uint32_t> h_tstart;
     DBuf<int64_t> d_T, d_Cprev, d_Rj, d_Cj, d_candP, d_candms;
     DBuf<uint32_t> d_candtile, d_candkind;
-    DBuf<unsigned long long> d_candkey;
+    DBuf<long long> d_candkey;
     // staging of host-memory batches
     DBuf<uint32_t> s_key, s_rank, s_val;
     DBuf<int64_t> s_lt, s_millis, s_mod;
     DBuf<uint8_t> s_flags;
     DBuf<uint32_t> s_out;
-    DBuf<unsigned long long> d_word;
+    DBuf<long long> d_word;
     // per-call plan (set by scan, used by later phases)
     uint32_t plan_R = 0;
     uint64_t plan_tiles = 0;
@@ -776,7 +789,7 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 }
 
 // ---- phases ---------------------------------------------------------------
-int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, unsigned long long* d_maxima) {
+int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima) {
     int st = validate_batch(home);
     if (st) return st;
     const uint32_t R = home->n_changesets;
@@ -792,7 +805,8 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, unsigned long 
     HIPALLOC(c->d_candkind.ensure(tiles + 1));
     HIPALLOC(c->d_candms.ensure(tiles + 1));
     if ((st = reset_misc(c))) return st;
-    HIPCHK(hipMemsetAsync(d_maxima, 0, std::max<uint32_t>(R, 1) * sizeof(unsigned long long), c->stream));
+    k_fill_i64<<<grid_for(std::max<uint32_t>(R, 1), 256), 256, 0, c->stream>>>(d_maxima, std::max<uint32_t>(R, 1),
+                                                                                 INT64_MIN);
     c->plan_R = R;
     c->plan_tiles = tiles;
     if (tiles) {
@@ -810,8 +824,8 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, unsigned long 
     return CRDT_OK;
 }
 
-int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const unsigned long long* d_maxima,
-                unsigned long long* d_event) {
+int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long long* d_maxima,
+                long long* d_event) {
     const uint32_t R = c->plan_R;
     if (!home || home->n_changesets != R) return CRDT_E_INVALID;
     int st;
@@ -820,7 +834,7 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const unsigne
     HIPALLOC(c->d_Cprev.ensure(R + 1));
     HIPALLOC(c->d_Rj.ensure(R + 1));
     HIPALLOC(c->d_Cj.ensure(R + 1));
-    HIPCHK(hipMemsetAsync(d_event, 0xFF, 4 * sizeof(unsigned long long), c->stream));
+    k_event_init<<<1, 64, 0, c->stream>>>(d_event);
     if (R) k_clock<<<1, 1024, 0, c->stream>>>(d_maxima, R, wall, c->canonical, c->d_Cprev.p, c->d_Rj.p,
                                               c->d_Cj.p, d_event);
     if (c->plan_tiles)
@@ -832,14 +846,14 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const unsigne
     return CRDT_OK;
 }
 
-int phase_resolve(crdt_ctx* c, unsigned long long* d_event) {
+int phase_resolve(crdt_ctx* c, long long* d_event) {
     k_resolve_local<<<1, 256, 0, c->stream>>>(c->d_misc, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
                                               c->d_candms.p, d_event);
     HIPCHK(hipGetLastError());
     return CRDT_OK;
 }
 
-int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const unsigned long long* d_event,
+int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long long* d_event,
                 uint8_t* win_flags, crdt_result* out, size_t ev_base) {
     int st = validate_batch(owned);
     if (st) return st;
@@ -1131,16 +1145,16 @@ int crdt_read_rows(crdt_ctx* c, const uint32_t* key_id, uint64_t n, int64_t* lt,
 int crdt_refresh_canonical(crdt_ctx* c, uint64_t n_rows, int64_t* out_lt) {
     if (!c || n_rows > c->cap) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(c->d_word.p, 0, sizeof(unsigned long long), c->stream));
+    k_fill_i64<<<1, 64, 0, c->stream>>>(c->d_word.p, 1, INT64_MIN);
     if (n_rows) {
         const unsigned g = std::min<unsigned>(grid_for(n_rows, 256), 2048);
         k_refresh<<<g, 256, 0, c->stream>>>(c->table, n_rows, c->d_word.p);
         HIPCHK(hipGetLastError());
     }
-    unsigned long long w = 0;
+    long long w = 0;
     HIPCHK(hipMemcpyAsync(&w, c->d_word.p, sizeof(w), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    const int64_t lt = (w == 0) ? 0 : dec(w);         // empty recordMap -> 0 (crdt.dart:118)
+    const int64_t lt = (w == INT64_MIN) ? 0 : (int64_t)w;  // empty recordMap -> 0 (crdt.dart:118)
     c->canonical = lt;                                 // fromLogicalTime(max, nodeId)
     if (out_lt) *out_lt = lt;
     return CRDT_OK;
@@ -1159,7 +1173,7 @@ int crdt_modified_since(crdt_ctx* c, uint64_t n_rows, int64_t since_lt, uint32_t
     k_ms_scan<<<1, 1024, 0, c->stream>>>(counts, nb, c->d_word.p);
     k_ms_write<<<nb, 256, 0, c->stream>>>(c->table, n_rows, since_lt, counts, c->s_out.p);
     HIPCHK(hipGetLastError());
-    unsigned long long total = 0;
+    long long total = 0;
     HIPCHK(hipMemcpyAsync(&total, c->d_word.p, sizeof(total), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (total) HIPCHK(hipMemcpy(out_ids, c->s_out.p, total * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1241,21 +1255,27 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
 int crdt_merge_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, uint64_t* d_maxima) {
     if (!c || !d_maxima) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    return phase_scan(c, home, wall, reinterpret_cast<unsigned long long*>(d_maxima));
+    int st = phase_scan(c, home, wall, reinterpret_cast<long long*>(d_maxima));
+    if (st) return st;
+    HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_maxima next
+    return CRDT_OK;
 }
 
 int crdt_merge_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const uint64_t* d_maxima,
                      uint64_t* d_event) {
     if (!c || !d_maxima || !d_event) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    return phase_clock(c, home, wall, reinterpret_cast<const unsigned long long*>(d_maxima),
-                       reinterpret_cast<unsigned long long*>(d_event));
+    int st = phase_clock(c, home, wall, reinterpret_cast<const long long*>(d_maxima),
+                         reinterpret_cast<long long*>(d_event));
+    if (st) return st;
+    HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_event[0] next
+    return CRDT_OK;
 }
 
 int crdt_merge_resolve(crdt_ctx* c, const crdt_batch* home, uint64_t* d_event) {
     if (!c || !d_event || !home || home->n_changesets != c->plan_R) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    int st = phase_resolve(c, reinterpret_cast<unsigned long long*>(d_event));
+    int st = phase_resolve(c, reinterpret_cast<long long*>(d_event));
     if (st) return st;
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
@@ -1267,7 +1287,7 @@ int crdt_merge_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const u
     HIPCHK(hipSetDevice(c->device));
     const bool timing = c->timing;
     c->timing = false;
-    int st = phase_apply(c, owned, wall, reinterpret_cast<const unsigned long long*>(d_event), win_flags, out, 0);
+    int st = phase_apply(c, owned, wall, reinterpret_cast<const long long*>(d_event), win_flags, out, 0);
     c->timing = timing;
     return st;
 }

@@ -157,11 +157,13 @@ int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint
  * crdt_merge() == scan -> clock -> resolve -> apply on one ctx.  With keys
  * sharded over G ranks, each rank scans the changesets it is home to (a batch
  * with all R changesets, non-home ones empty), and between phases the host
- * all-reduces the device words (RCCL over xGMI):
- *   d_maxima [R]  u64 : MAX all-reduce after scan
- *   d_event  [4]  u64 : MIN all-reduce of d_event[0] after clock, MAX of d_event[1..3]
- *                       after resolve
- * then applies the records it owns (any rank: owned batch, same n_changesets). */
+ * all-reduces the device words (RCCL over xGMI); all are plain signed int64:
+ *   d_maxima [R] : MAX all-reduce after scan   (M_j = max lt of changeset j; INT64_MIN: empty)
+ *   d_event  [4] : MIN all-reduce of d_event[0] after clock (first exception, (j << 40) | i;
+ *                  INT64_MAX: none), then MAX all-reduce of d_event[1..3] after resolve
+ *                  (canonical at the failure, kind, Hlc.millis of the failing record)
+ * then applies the records it owns (any rank: owned batch, same n_changesets).
+ * scan and clock synchronise the ctx stream before returning. */
 int crdt_merge_scan(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis, uint64_t* d_maxima);
 int crdt_merge_clock(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis,
                      const uint64_t* d_maxima, uint64_t* d_event);

@@ -149,3 +149,78 @@ def test_reserve_preserves_rows(gpu_device):
     t.reserve(100_000)
     lt, rank, val, mod = t.read_rows(np.array([3, 99_999], np.uint32))
     assert (lt[0], rank[0], val[0], mod[0]) == (42, 1, 7, 43) and mod[1] < 0
+
+
+def _sharded_gpu_worker(rank, world, port, case_kw, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.dist import sharded_merge, torch_reducers
+    from tests.test_dist_cpu import _split
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = make_case(**case_kw)
+        cap = -(-case["n_ids"] // world)
+        t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
+        loc = case["local"]
+        ids = np.arange(case["n_local"])
+        mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
+        if mine.any():
+            t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
+                       loc["val"][mine], loc["mod"][mine])
+        t.canonical = case["c0"]
+        owned, home, idx = _split(case, world, rank)
+        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        owned_d = (dev(owned[0]), dev(owned[1]), dev(owned[2]), dev(owned[3]), owned[4], None)
+        home_d = (None, dev(home[1]), dev(home[2]), None, home[4], dev(home[5]))
+        R = len(case["offsets"]) - 1
+        d_max = torch.zeros(max(R, 1), dtype=torch.int64, device="cuda")
+        d_ev = torch.zeros(4, dtype=torch.int64, device="cuda")
+        flags = torch.zeros(max(len(idx), 1), dtype=torch.uint8, device="cuda")
+        red_max, red_min = torch_reducers(dist)
+        res = sharded_merge(t, home_d, owned_d, case["wall"], d_max, d_ev, red_max, red_min, win_flags=flags)
+        lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
+        q.put((rank, res, lt, rk, val, mod, idx, flags[:len(idx)].cpu().numpy()))
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
+def test_two_rank_sharded_on_device(gpu_device, name):
+    """The device phase API under the multi-rank protocol (2 processes on one GPU, gloo)."""
+    import torch.multiprocessing as mp
+
+    from tests.test_dist_cpu import _free_port
+    kw = dict(CASE_SPECS)[name]
+    case = make_case(**kw)
+    orows, ores, oflags = oracle_run(case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_gpu_worker, args=(r, 2, port, kw, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    flags = np.zeros(len(case["key"]), np.uint8)
+    tot = [0, 0]
+    for rank, res, lt, rk, val, mod, idx, fl in outs:
+        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
+            assert res[f] == ores[f], (name, rank, f)
+        tot[0] += res["n_present"]
+        tot[1] += res["n_won"]
+        flags[idx] = fl
+        keys = np.arange(case["n_ids"])
+        mine = keys % 2 == rank
+        slots = keys[mine] // 2
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a[slots], orows[f][mine]), f
+    assert tot == [ores["n_present"], ores["n_won"]]
+    assert np.array_equal(flags, oflags)
