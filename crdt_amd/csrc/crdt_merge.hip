@@ -38,7 +38,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kTile = kScanThreads * kScanItems; // 4096 records per scan tile
 constexpr int kApplyThreads = 256;
-constexpr int kApplyItems = 4;
+constexpr int kApplyItems = 4;          // consecutive records per thread
 constexpr int kApplyPerBlock = kApplyThreads * kApplyItems;
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
@@ -52,15 +52,42 @@ constexpr int64_t kLowBits = 40;
 constexpr int64_t kLowMask = (1ll << kLowBits) - 1;
 constexpr int64_t kEvNone = INT64_MAX;
 
-// One device row per key id.  32-byte aligned: a random access is one 32-B sector.
+// One device row per key id, 32 B, 32-B aligned.  Everything the merge decision
+// needs sits in the first 16 B, so the gather of a row is ONE dwordx4 (random
+// row accesses are request-rate bound: tools/ubench_gather.hip):
+//   [0:8)  lt      Record.hlc.logicalTime
+//   [8:12) rank    Record.hlc.nodeId rank
+//   [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the
+//                  visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
+//   [16:20) mod_lo low word of modified
+//   [20:24) val    Record.value handle
+//   [24:32) aux    reserved (zero)
 struct alignas(32) Row {
-    int64_t lt;      // Record.hlc.logicalTime
-    uint32_t rank;   // Record.hlc.nodeId rank
-    uint32_t val;    // Record.value handle
-    int64_t mod;     // Record.modified.logicalTime (< 0: invisible to merge / recordMap)
-    int64_t aux;     // reserved (zero)
+    int64_t lt;
+    uint32_t rank;
+    int32_t mod_hi;
+    uint32_t mod_lo;
+    uint32_t val;
+    int64_t aux;
 };
 static_assert(sizeof(Row) == 32, "row layout");
+
+__host__ __device__ inline int64_t row_mod(const Row& r) {
+    return (int64_t)(((uint64_t)(uint32_t)r.mod_hi << 32) | r.mod_lo);
+}
+__host__ __device__ inline Row make_row(int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
+    Row r;
+    r.lt = lt; r.rank = rank; r.mod_hi = (int32_t)((uint64_t)mod >> 32); r.mod_lo = (uint32_t)mod;
+    r.val = val; r.aux = 0;
+    return r;
+}
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+__device__ inline void store_row(Row* dst, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
+    u32x8 v;                       // one 32-B vector store = two aligned dwordx4
+    v.s0 = (uint32_t)lt; v.s1 = (uint32_t)((uint64_t)lt >> 32); v.s2 = rank; v.s3 = (uint32_t)((uint64_t)mod >> 32);
+    v.s4 = (uint32_t)mod; v.s5 = val; v.s6 = 0u; v.s7 = 0u;
+    *reinterpret_cast<u32x8*>(dst) = v;
+}
 
 // Device-side per-call words.
 struct Misc {
@@ -72,6 +99,9 @@ struct Misc {
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
 __host__ __device__ inline int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
@@ -362,68 +392,90 @@ __global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64
 }
 
 // =============================================================================
-// K2 — k_apply: one changeset (crdt.dart:83-90).  Winner <=> local absent
-// (mod < 0) or local.hlc < remote.hlc in (lt, rank) order; equal keeps local.
+// K2 — k_apply: one changeset (crdt.dart:83-90).  Winner <=> local row invisible
+// (mod < 0, incl. never written) or local.hlc < remote.hlc in (lt, rank) order;
+// equal keeps local.  Each thread owns 4 consecutive records of a 4-aligned
+// group: 16-B stream loads, then all four row gathers (one dwordx4 each) are in
+// flight before any is used — no per-record branch around a load.
 // =============================================================================
+struct Quad {
+    uint32_t k[4], r[4], v[4];
+    int64_t l[4];
+    bool in[4];
+};
+
+template <bool VEC>
+__device__ inline void load_quad(Quad& Q, const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
+                                 const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val,
+                                 uint64_t i0, uint64_t beg, uint64_t end)
+{
+    if (VEC && i0 >= beg && i0 + 4 <= end) {
+        const u32x4 kk = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(key + i0));
+        const u32x4 rr = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rank + i0));
+        const u32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(val + i0));
+        const i64x2 l01 = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(lt + i0));
+        const i64x2 l23 = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(lt + i0 + 2));
+        Q.k[0] = kk.x; Q.k[1] = kk.y; Q.k[2] = kk.z; Q.k[3] = kk.w;
+        Q.r[0] = rr.x; Q.r[1] = rr.y; Q.r[2] = rr.z; Q.r[3] = rr.w;
+        Q.v[0] = vv.x; Q.v[1] = vv.y; Q.v[2] = vv.z; Q.v[3] = vv.w;
+        Q.l[0] = l01.x; Q.l[1] = l01.y; Q.l[2] = l23.x; Q.l[3] = l23.y;
+        Q.in[0] = Q.in[1] = Q.in[2] = Q.in[3] = true;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t i = i0 + q;
+            Q.in[q] = i >= beg && i < end;
+            const uint64_t ii = Q.in[q] ? i : beg;        // always a valid address
+            Q.k[q] = key[ii]; Q.l[q] = lt[ii]; Q.r[q] = rank[ii]; Q.v[q] = val[ii];
+        }
+    }
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kApplyThreads) void k_apply(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
     const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
     uint64_t end, uint32_t j, Row* __restrict__ table, uint64_t cap,
     const int64_t* __restrict__ Rj, Misc* __restrict__ misc, uint8_t* __restrict__ flags)
 {
-    if (j >= misc->stop) return;
+    if (j >= misc->stop) return;                          // uniform: changeset past the stop point
     const int64_t stamp = Rj[j];
-    const uint64_t base = beg + (uint64_t)blockIdx.x * kApplyPerBlock;
-    uint32_t k[kApplyItems], r[kApplyItems], v[kApplyItems];
-    int64_t l[kApplyItems];
-    bool in[kApplyItems];
+    const uint64_t a0 = VEC ? (beg & ~3ull) : beg;
+    const uint64_t i0 = a0 + ((uint64_t)blockIdx.x * kApplyThreads + threadIdx.x) * 4;
+    Quad Q;
+    load_quad<VEC>(Q, key, lt, rank, val, i0, beg, end);
+    uint4 h[4];
+    bool ok[4];
 #pragma unroll
-    for (int q = 0; q < kApplyItems; ++q) {
-        const uint64_t i = base + (uint64_t)q * kApplyThreads + threadIdx.x;
-        in[q] = i < end;
-        if (in[q]) {
-            k[q] = __builtin_nontemporal_load(key + i);
-            l[q] = __builtin_nontemporal_load(lt + i);
-            r[q] = __builtin_nontemporal_load(rank + i);
-            v[q] = __builtin_nontemporal_load(val + i);
-        }
-    }
-    uint4 a[kApplyItems], bq[kApplyItems];
-    bool ok[kApplyItems];
-#pragma unroll
-    for (int q = 0; q < kApplyItems; ++q) {
-        ok[q] = in[q] && k[q] < cap;
-        if (ok[q]) {
-            const uint4* p = reinterpret_cast<const uint4*>(table + k[q]);
-            a[q] = p[0];
-            bq[q] = p[1];
-        }
+    for (int q = 0; q < 4; ++q) {                        // four independent gathers in flight
+        ok[q] = Q.in[q] && Q.k[q] < cap;
+        const uint64_t row = ok[q] ? Q.k[q] : 0;
+        h[q] = *reinterpret_cast<const uint4*>(table + row);
     }
     int npres = 0, nwon = 0;
     bool bad = false;
+    uint32_t fl = 0;
 #pragma unroll
-    for (int q = 0; q < kApplyItems; ++q) {
-        bool win = false;
-        if (ok[q]) {
-            const int64_t llt = (int64_t)(((uint64_t)a[q].y << 32) | a[q].x);
-            const uint32_t lrank = a[q].z;
-            const int64_t lmod = (int64_t)(((uint64_t)bq[q].y << 32) | bq[q].x);
-            const bool present = lmod >= 0;
-            win = !present || l[q] > llt || (l[q] == llt && r[q] > lrank);
-            npres += present;
-            if (win) {
-                uint4* p = reinterpret_cast<uint4*>(table + k[q]);
-                p[0] = make_uint4((uint32_t)l[q], (uint32_t)((uint64_t)l[q] >> 32), r[q], v[q]);
-                p[1] = make_uint4((uint32_t)stamp, (uint32_t)((uint64_t)stamp >> 32), 0u, 0u);
-                ++nwon;
-            }
-        } else if (in[q]) {
-            bad = true;
+    for (int q = 0; q < 4; ++q) {
+        const int64_t llt = (int64_t)(((uint64_t)h[q].y << 32) | h[q].x);
+        const bool present = (int32_t)h[q].w >= 0;
+        const bool win = ok[q] && (!present || Q.l[q] > llt || (Q.l[q] == llt && Q.r[q] > h[q].z));
+        npres += ok[q] && present;
+        nwon += win;
+        bad |= Q.in[q] && !ok[q];
+        if (win) store_row(table + Q.k[q], Q.l[q], Q.r[q], Q.v[q], stamp);
+        fl |= (uint32_t)win << (8 * q);
+    }
+    if (flags) {
+        if (VEC && Q.in[0] && Q.in[3]) {
+            *reinterpret_cast<uint32_t*>(flags + i0) = fl;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (Q.in[q]) flags[i0 + q] = (uint8_t)(fl >> (8 * q));
         }
-        if (flags && in[q]) flags[base + (uint64_t)q * kApplyThreads + threadIdx.x] = win ? 1 : 0;
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
-    // wave-level counts, one striped atomic per wave
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         npres += __shfl_xor(npres, off, 64);
@@ -446,9 +498,7 @@ __global__ __launch_bounds__(256) void k_put_rows(
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    Row row;
-    row.lt = lt[i]; row.rank = rank[i]; row.val = val[i]; row.mod = mod[i]; row.aux = 0;
-    table[k] = row;
+    table[k] = make_row(lt[i], rank[i], val[i], mod[i]);
 }
 
 // put/putAll rows (crdt.dart:41-42, 51-53): hlc = modified = the one send() result.
@@ -460,9 +510,7 @@ __global__ __launch_bounds__(256) void k_put_stamped(
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    Row row;
-    row.lt = stamp; row.rank = local_rank; row.val = val[i]; row.mod = stamp; row.aux = 0;
-    table[k] = row;
+    table[k] = make_row(stamp, local_rank, val[i], stamp);
 }
 
 __global__ __launch_bounds__(256) void k_read_rows(
@@ -478,7 +526,7 @@ __global__ __launch_bounds__(256) void k_read_rows(
     if (lt) lt[i] = row.lt;
     if (rank) rank[i] = row.rank;
     if (val) val[i] = row.val;
-    if (mod) mod[i] = row.mod;
+    if (mod) mod[i] = row_mod(row);
 }
 
 // refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
@@ -490,7 +538,7 @@ __global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, 
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const Row row = table[i];
-        if (row.mod >= 0) m = imax(m, row.lt);
+        if (row.mod_hi >= 0) m = imax(m, row.lt);
     }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = m;
@@ -511,7 +559,7 @@ __global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table,
     int c = 0;
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        if (i < n) c += !(table[i].mod < since);
+        if (i < n) c += !(row_mod(table[i]) < since);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -568,7 +616,7 @@ __global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table,
     uint32_t run = offsets[blockIdx.x];
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        const bool keep = i < n && !(table[i].mod < since);
+        const bool keep = i < n && !(row_mod(table[i]) < since);
         const unsigned long long b = __ballot(keep);
         const int before = __popcll(b & ((1ull << lane) - 1));
         if (lane == 0) s_wave[w] = __popcll(b);
@@ -686,6 +734,7 @@ namespace {
     } while (0)
 
 inline unsigned grid_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 hipError_t ensure_events(crdt_ctx* c, size_t n) {
     while (c->events.size() < n) {
@@ -875,13 +924,21 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     ev_record(c, ev_base);
     c->launched.clear();
+    const bool vec = aligned16(cols.key) && aligned16(cols.lt) && aligned16(cols.rank) && aligned16(cols.val) &&
+                     ((uintptr_t)dflags & 3) == 0;
     for (uint32_t j = 0; j < R; ++j) {
         const uint64_t b = owned->offsets[j], e = owned->offsets[j + 1];
         if (e == b) continue;
         c->launched.push_back(j);
         if (c->timing) ev_record(c, ev_base + 1 + 2 * (size_t)j);
-        k_apply<<<grid_for(e - b, kApplyPerBlock), kApplyThreads, 0, c->stream>>>(
-            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        const uint64_t a0 = vec ? (b & ~3ull) : b;
+        const unsigned g = grid_for((e - a0 + 3) / 4, kApplyThreads);
+        if (vec)
+            k_apply<true><<<g, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        else
+            k_apply<false><<<g, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                               c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
         if (c->timing) ev_record(c, ev_base + 2 + 2 * (size_t)j);
     }
     HIPCHK(hipGetLastError());

@@ -77,8 +77,9 @@ def test_device_resident_columns(gpu_device):
 
 def test_large_single_changeset(gpu_device):
     """One changeset of 1M records: many scan tiles, many apply blocks."""
+    from tests._cases import WALL
     res = compare_with_oracle(make_case(seed=78, R=1, per_cs=1_000_000, n_local=1_200_000, n_new=800_000,
-                                        millis_span=1 << 16))
+                                        millis_span=1 << 16, base=WALL - 70_000))
     assert res["status"] == 0 and res["n_won"] > 0
 
 
