@@ -119,7 +119,7 @@ def main():
         reset()
         step()
     table.set_timing(True)
-    step_ms, apply_ms, apply_launches, scan_ms, clock_ms, dev_ms = [], 0.0, 0, 0.0, 0.0, 0.0
+    step_ms, apply_ms, apply_launches, apply_total, scan_ms, clock_ms, dev_ms = [], 0.0, 0, 0, 0.0, 0.0, 0.0
     res = None
     for _ in range(args.steps):
         reset()
@@ -136,6 +136,7 @@ def main():
         tm = table.timing()
         apply_ms += tm["apply_ms"]
         apply_launches += tm["apply_launches"]
+        apply_total += tm["apply_total"]
         scan_ms += tm["scan_ms"]
         clock_ms += tm["clock_ms"]
         dev_ms += tm["total_ms"]
@@ -148,12 +149,15 @@ def main():
     # ---- per-kernel roofline of K2 (apply): algorithmic bytes / event-timed duration
     n_owned = int(wl["owned_offsets"][-1])
     kb = 20 * n_owned + 12 * res["n_present"] + 24 * res["n_won"]          # per step, this rank
-    achieved = kb * args.steps / (apply_ms / 1e3) if apply_ms > 0 else 0.0
-    avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)
+    launches_per_step = max(apply_total // max(args.steps, 1), 1)
+    alg_per_launch = kb / launches_per_step
+    avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)                  # HIP events, sampled launches
+    achieved = alg_per_launch / (avg_launch_us / 1e6) if apply_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
                 "kernel": "k_apply (K2)", "avg_launch_us": round(avg_launch_us, 2),
-                "alg_bytes_per_launch": int(kb / max(apply_launches // max(args.steps, 1), 1))}
+                "alg_bytes_per_launch": int(alg_per_launch), "launches_per_step": launches_per_step,
+                "launches_timed": apply_launches}
     # traffic (PMC) is filled from the committed rocprofv3 --pmc pass of this command, when present
     pmc = os.path.join(ROOT, "profiles", "pmc_k_apply.json")
     if os.path.exists(pmc) and world == 1 and args.config == "fanin":
@@ -195,7 +199,8 @@ def main():
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
-                         "apply_kernels": round(apply_ms / args.steps, 3), "apply_launches": apply_launches // args.steps,
+                         "apply_kernels_est": round(avg_launch_us * launches_per_step / 1e3, 3),
+                         "apply_launches": launches_per_step,
                          "device_total": round(dev_ms / args.steps, 3)},
     }
     if rank == 0:

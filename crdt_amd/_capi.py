@@ -47,10 +47,10 @@ class CrdtResult(ctypes.Structure):
 class CrdtTiming(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("clock_ms", ctypes.c_double),
                 ("apply_ms", ctypes.c_double), ("apply_launches", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32), ("total_ms", ctypes.c_double)]
+                ("apply_total", ctypes.c_uint32), ("total_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 _P = ctypes.c_void_p

@@ -42,6 +42,7 @@ constexpr int kApplyItems = 4;          // consecutive records per thread
 constexpr int kApplyPerBlock = kApplyThreads * kApplyItems;
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
+constexpr uint32_t kTimingStride = 16;          // time every 16th apply launch
 
 // Collective words are plain signed int64 so an RCCL MAX / MIN all-reduce combines them:
 //   maxima[j]  = M_j, INT64_MIN when changeset j is empty (or not homed here)
@@ -397,41 +398,9 @@ __global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64
 // equal keeps local.  Each thread owns 4 consecutive records of a 4-aligned
 // group: 16-B stream loads, then all four row gathers (one dwordx4 each) are in
 // flight before any is used — no per-record branch around a load.
+// (A blocked 4-consecutive-records layout with dwordx4 stream loads measured the
+// same on the fan-in and 20 % slower on cfg2, whose new ids are consecutive.)
 // =============================================================================
-struct Quad {
-    uint32_t k[4], r[4], v[4];
-    int64_t l[4];
-    bool in[4];
-};
-
-template <bool VEC>
-__device__ inline void load_quad(Quad& Q, const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
-                                 const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val,
-                                 uint64_t i0, uint64_t beg, uint64_t end)
-{
-    if (VEC && i0 >= beg && i0 + 4 <= end) {
-        const u32x4 kk = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(key + i0));
-        const u32x4 rr = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rank + i0));
-        const u32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(val + i0));
-        const i64x2 l01 = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(lt + i0));
-        const i64x2 l23 = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(lt + i0 + 2));
-        Q.k[0] = kk.x; Q.k[1] = kk.y; Q.k[2] = kk.z; Q.k[3] = kk.w;
-        Q.r[0] = rr.x; Q.r[1] = rr.y; Q.r[2] = rr.z; Q.r[3] = rr.w;
-        Q.v[0] = vv.x; Q.v[1] = vv.y; Q.v[2] = vv.z; Q.v[3] = vv.w;
-        Q.l[0] = l01.x; Q.l[1] = l01.y; Q.l[2] = l23.x; Q.l[3] = l23.y;
-        Q.in[0] = Q.in[1] = Q.in[2] = Q.in[3] = true;
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t i = i0 + q;
-            Q.in[q] = i >= beg && i < end;
-            const uint64_t ii = Q.in[q] ? i : beg;        // always a valid address
-            Q.k[q] = key[ii]; Q.l[q] = lt[ii]; Q.r[q] = rank[ii]; Q.v[q] = val[ii];
-        }
-    }
-}
-
-template <bool VEC>
 __global__ __launch_bounds__(kApplyThreads) void k_apply(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
     const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
@@ -440,40 +409,43 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
 {
     if (j >= misc->stop) return;                          // uniform: changeset past the stop point
     const int64_t stamp = Rj[j];
-    const uint64_t a0 = VEC ? (beg & ~3ull) : beg;
-    const uint64_t i0 = a0 + ((uint64_t)blockIdx.x * kApplyThreads + threadIdx.x) * 4;
-    Quad Q;
-    load_quad<VEC>(Q, key, lt, rank, val, i0, beg, end);
-    uint4 h[4];
-    bool ok[4];
+    // striped: record q of this thread = base + q * 256 + tid, so a wave's q-th
+    // access covers 64 consecutive records (coalesced streams; consecutive new ids
+    // give coalesced rows)
+    const uint64_t base = beg + (uint64_t)blockIdx.x * kApplyPerBlock + threadIdx.x;
+    uint32_t k[kApplyItems], r[kApplyItems], v[kApplyItems];
+    int64_t l[kApplyItems];
+    bool in[kApplyItems];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {                        // four independent gathers in flight
-        ok[q] = Q.in[q] && Q.k[q] < cap;
-        const uint64_t row = ok[q] ? Q.k[q] : 0;
+    for (int q = 0; q < kApplyItems; ++q) {
+        const uint64_t i = base + (uint64_t)q * kApplyThreads;
+        in[q] = i < end;
+        const uint64_t ii = in[q] ? i : beg;             // always a valid address, no branch
+        k[q] = __builtin_nontemporal_load(key + ii);
+        l[q] = __builtin_nontemporal_load(lt + ii);
+        r[q] = __builtin_nontemporal_load(rank + ii);
+        v[q] = __builtin_nontemporal_load(val + ii);
+    }
+    uint4 h[kApplyItems];
+    bool ok[kApplyItems];
+#pragma unroll
+    for (int q = 0; q < kApplyItems; ++q) {              // all gathers in flight, one dwordx4 each
+        ok[q] = in[q] && k[q] < cap;
+        const uint64_t row = ok[q] ? k[q] : 0;
         h[q] = *reinterpret_cast<const uint4*>(table + row);
     }
     int npres = 0, nwon = 0;
     bool bad = false;
-    uint32_t fl = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kApplyItems; ++q) {
         const int64_t llt = (int64_t)(((uint64_t)h[q].y << 32) | h[q].x);
         const bool present = (int32_t)h[q].w >= 0;
-        const bool win = ok[q] && (!present || Q.l[q] > llt || (Q.l[q] == llt && Q.r[q] > h[q].z));
+        const bool win = ok[q] && (!present || l[q] > llt || (l[q] == llt && r[q] > h[q].z));
         npres += ok[q] && present;
         nwon += win;
-        bad |= Q.in[q] && !ok[q];
-        if (win) store_row(table + Q.k[q], Q.l[q], Q.r[q], Q.v[q], stamp);
-        fl |= (uint32_t)win << (8 * q);
-    }
-    if (flags) {
-        if (VEC && Q.in[0] && Q.in[3]) {
-            *reinterpret_cast<uint32_t*>(flags + i0) = fl;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (Q.in[q]) flags[i0 + q] = (uint8_t)(fl >> (8 * q));
-        }
+        bad |= in[q] && !ok[q];
+        if (win) store_row(table + k[q], l[q], r[q], v[q], stamp);
+        if (flags && in[q]) flags[base + (uint64_t)q * kApplyThreads] = win ? 1 : 0;
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
 #pragma unroll
@@ -715,6 +687,7 @@ struct crdt_ctx {
     bool timing = false;
     std::vector<hipEvent_t> events;
     std::vector<uint32_t> launched;
+    uint32_t apply_total = 0;
     crdt_timing last_timing{};
 };
 
@@ -924,22 +897,19 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     ev_record(c, ev_base);
     c->launched.clear();
-    const bool vec = aligned16(cols.key) && aligned16(cols.lt) && aligned16(cols.rank) && aligned16(cols.val) &&
-                     ((uintptr_t)dflags & 3) == 0;
+    uint32_t nl = 0;
+    c->apply_total = 0;
     for (uint32_t j = 0; j < R; ++j) {
         const uint64_t b = owned->offsets[j], e = owned->offsets[j + 1];
         if (e == b) continue;
-        c->launched.push_back(j);
-        if (c->timing) ev_record(c, ev_base + 1 + 2 * (size_t)j);
-        const uint64_t a0 = vec ? (b & ~3ull) : b;
-        const unsigned g = grid_for((e - a0 + 3) / 4, kApplyThreads);
-        if (vec)
-            k_apply<true><<<g, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
-                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
-        else
-            k_apply<false><<<g, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
-                                                               c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
-        if (c->timing) ev_record(c, ev_base + 2 + 2 * (size_t)j);
+        // HIP-event timing of a sample of the launches (every kTimingStride-th): per-launch
+        // durations without perturbing the rest of the stream
+        const bool timed = c->timing && (nl++ % kTimingStride) == 0;
+        c->apply_total++;
+        if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
+        k_apply<<<grid_for(e - b, kApplyPerBlock), kApplyThreads, 0, c->stream>>>(
+            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        if (timed) ev_record(c, ev_base + 2 + 2 * (size_t)j);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
@@ -972,6 +942,7 @@ void collect_timing(crdt_ctx* c, uint32_t R, bool full) {
                 t.apply_launches++;
             }
         }
+        t.apply_total = c->apply_total;
         const size_t last = 3 + 2 * (size_t)R + 1;
         if (hipEventElapsedTime(&ms, c->events[0], c->events[last]) == hipSuccess) t.total_ms = ms;
     }
