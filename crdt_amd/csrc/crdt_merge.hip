@@ -53,47 +53,41 @@ constexpr int64_t kLowBits = 40;
 constexpr int64_t kLowMask = (1ll << kLowBits) - 1;
 constexpr int64_t kEvNone = INT64_MAX;
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef long long i64x2 __attribute__((ext_vector_type(2)));
-
-// Per key id the table keeps two arrays (struct of arrays by access pattern):
-//   dec[k] 16 B, 16-B aligned — everything the merge DECISION reads, so the random
-//          gather of a key is ONE dwordx4 into a 4.3 GB array (2^28 keys; 8 keys per
-//          128-B L2 line; the Zipf-hot keys fit the 256 MB Infinity Cache):
-//            [0:8) lt = Record.hlc.logicalTime, [8:12) rank = Record.hlc.nodeId rank,
-//            [12:16) mod_hi = high word of Record.modified.logicalTime; its sign is the
-//            visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
-//   pay[k] 8 B — written by winners, read only by the API: {mod_lo, val}.
-// Random 16-B gathers are request-rate bound and run faster on the smaller array
-// (tools/ubench_gather.hip: ~30 G rows/s at 8 GB vs ~41-47 at 4 GB).
-struct alignas(16) Dec {
+// One device row per key id, 32 B, 32-B aligned.  Everything the merge decision
+// needs sits in the first 16 B, so the gather of a row is ONE dwordx4 (random
+// row accesses are request-rate bound: tools/ubench_gather.hip):
+//   [0:8)  lt      Record.hlc.logicalTime
+//   [8:12) rank    Record.hlc.nodeId rank
+//   [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the
+//                  visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
+//   [16:20) mod_lo low word of modified
+//   [20:24) val    Record.value handle
+//   [24:32) aux    reserved (zero)
+struct alignas(32) Row {
     int64_t lt;
     uint32_t rank;
     int32_t mod_hi;
-};
-struct alignas(8) Pay {
     uint32_t mod_lo;
     uint32_t val;
+    int64_t aux;
 };
-static_assert(sizeof(Dec) == 16 && sizeof(Pay) == 8, "table layout");
+static_assert(sizeof(Row) == 32, "row layout");
 
-struct Table {
-    Dec* dec;
-    Pay* pay;
-    uint64_t cap;
-};
-
-__host__ __device__ inline int64_t join_mod(int32_t hi, uint32_t lo) {
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | lo);
+__host__ __device__ inline int64_t row_mod(const Row& r) {
+    return (int64_t)(((uint64_t)(uint32_t)r.mod_hi << 32) | r.mod_lo);
 }
-__device__ inline void store_row(const Table& t, uint64_t k, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
-    u32x4 d;
-    d.x = (uint32_t)lt; d.y = (uint32_t)((uint64_t)lt >> 32); d.z = rank; d.w = (uint32_t)((uint64_t)mod >> 32);
-    *reinterpret_cast<u32x4*>(t.dec + k) = d;
-    u32x2 p;
-    p.x = (uint32_t)mod; p.y = val;
-    *reinterpret_cast<u32x2*>(t.pay + k) = p;
+__host__ __device__ inline Row make_row(int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
+    Row r;
+    r.lt = lt; r.rank = rank; r.mod_hi = (int32_t)((uint64_t)mod >> 32); r.mod_lo = (uint32_t)mod;
+    r.val = val; r.aux = 0;
+    return r;
+}
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+__device__ inline void store_row(Row* dst, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
+    u32x8 v;                       // one 32-B vector store = two aligned dwordx4
+    v.s0 = (uint32_t)lt; v.s1 = (uint32_t)((uint64_t)lt >> 32); v.s2 = rank; v.s3 = (uint32_t)((uint64_t)mod >> 32);
+    v.s4 = (uint32_t)mod; v.s5 = val; v.s6 = 0u; v.s7 = 0u;
+    *reinterpret_cast<u32x8*>(dst) = v;
 }
 
 // Device-side per-call words.
@@ -107,6 +101,8 @@ struct Misc {
     unsigned long long won[kCounterSlots];
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
 __host__ __device__ inline int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
@@ -408,11 +404,10 @@ __global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64
 __global__ __launch_bounds__(kApplyThreads) void k_apply(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
     const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
-    uint64_t end, uint32_t j, Table table,
+    uint64_t end, uint32_t j, Row* __restrict__ table, uint64_t cap,
     const int64_t* __restrict__ Rj, Misc* __restrict__ misc, uint8_t* __restrict__ flags)
 {
     if (j >= misc->stop) return;                          // uniform: changeset past the stop point
-    const uint64_t cap = table.cap;
     const int64_t stamp = Rj[j];
     // striped: record q of this thread = base + q * 256 + tid, so a wave's q-th
     // access covers 64 consecutive records (coalesced streams; consecutive new ids
@@ -437,7 +432,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     for (int q = 0; q < kApplyItems; ++q) {              // all gathers in flight, one dwordx4 each
         ok[q] = in[q] && k[q] < cap;
         const uint64_t row = ok[q] ? k[q] : 0;
-        h[q] = *reinterpret_cast<const uint4*>(table.dec + row);
+        h[q] = *reinterpret_cast<const uint4*>(table + row);
     }
     int npres = 0, nwon = 0;
     bool bad = false;
@@ -449,7 +444,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
         npres += ok[q] && present;
         nwon += win;
         bad |= in[q] && !ok[q];
-        if (win) store_row(table, k[q], l[q], r[q], v[q], stamp);
+        if (win) store_row(table + k[q], l[q], r[q], v[q], stamp);
         if (flags && in[q]) flags[base + (uint64_t)q * kApplyThreads] = win ? 1 : 0;
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
@@ -468,55 +463,54 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
 // ----------------------------------------------------------------- SPI kernels
 __global__ __launch_bounds__(256) void k_put_rows(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
-    const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Table table,
-    Misc* __restrict__ misc)
+    const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Row* __restrict__ table,
+    uint64_t cap, Misc* __restrict__ misc)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
-    if (k >= table.cap) { atomicOr(&misc->err, 1u); return; }
-    store_row(table, k, lt[i], rank[i], val[i], mod[i]);
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    table[k] = make_row(lt[i], rank[i], val[i], mod[i]);
 }
 
 // put/putAll rows (crdt.dart:41-42, 51-53): hlc = modified = the one send() result.
 __global__ __launch_bounds__(256) void k_put_stamped(
     const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n, int64_t stamp,
-    uint32_t local_rank, Table table, Misc* __restrict__ misc)
+    uint32_t local_rank, Row* __restrict__ table, uint64_t cap, Misc* __restrict__ misc)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
-    if (k >= table.cap) { atomicOr(&misc->err, 1u); return; }
-    store_row(table, k, stamp, local_rank, val[i], stamp);
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    table[k] = make_row(stamp, local_rank, val[i], stamp);
 }
 
 __global__ __launch_bounds__(256) void k_read_rows(
-    const uint32_t* __restrict__ key, uint64_t n, Table table,
+    const uint32_t* __restrict__ key, uint64_t n, const Row* __restrict__ table, uint64_t cap,
     int64_t* __restrict__ lt, uint32_t* __restrict__ rank, uint32_t* __restrict__ val,
     int64_t* __restrict__ mod, Misc* __restrict__ misc)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
-    if (k >= table.cap) { atomicOr(&misc->err, 1u); return; }
-    const Dec d = table.dec[k];
-    const Pay p = table.pay[k];
-    if (lt) lt[i] = d.lt;
-    if (rank) rank[i] = d.rank;
-    if (val) val[i] = p.val;
-    if (mod) mod[i] = join_mod(d.mod_hi, p.mod_lo);
+    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
+    const Row row = table[k];
+    if (lt) lt[i] = row.lt;
+    if (rank) rank[i] = row.rank;
+    if (val) val[i] = row.val;
+    if (mod) mod[i] = row_mod(row);
 }
 
 // refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
-__global__ __launch_bounds__(256) void k_refresh(const Dec* __restrict__ dec, uint64_t n,
+__global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, uint64_t n,
                                                  long long* __restrict__ out)
 {
     __shared__ int64_t s[4];
     int64_t m = INT64_MIN;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const Dec d = dec[i];
-        if (d.mod_hi >= 0) m = imax(m, d.lt);
+        const Row row = table[i];
+        if (row.mod_hi >= 0) m = imax(m, row.lt);
     }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = m;
@@ -529,7 +523,7 @@ __global__ __launch_bounds__(256) void k_refresh(const Dec* __restrict__ dec, ui
 
 // recordMap(modifiedSince) (map_crdt.dart:42-45): order-preserving compaction.
 constexpr int kMsPerBlock = 1024;
-__global__ __launch_bounds__(256) void k_ms_count(Table table, uint64_t n, int64_t since,
+__global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table, uint64_t n, int64_t since,
                                                   uint32_t* __restrict__ counts)
 {
     __shared__ int s[4];
@@ -537,7 +531,7 @@ __global__ __launch_bounds__(256) void k_ms_count(Table table, uint64_t n, int64
     int c = 0;
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        if (i < n) c += !(join_mod(table.dec[i].mod_hi, table.pay[i].mod_lo) < since);
+        if (i < n) c += !(row_mod(table[i]) < since);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -584,7 +578,7 @@ __global__ __launch_bounds__(1024) void k_ms_scan(uint32_t* __restrict__ counts,
     if (tid == 0) *total = (long long)s_carry;
 }
 
-__global__ __launch_bounds__(256) void k_ms_write(Table table, uint64_t n, int64_t since,
+__global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table, uint64_t n, int64_t since,
                                                   const uint32_t* __restrict__ offsets,
                                                   uint32_t* __restrict__ out)
 {
@@ -594,7 +588,7 @@ __global__ __launch_bounds__(256) void k_ms_write(Table table, uint64_t n, int64
     uint32_t run = offsets[blockIdx.x];
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        const bool keep = i < n && !(join_mod(table.dec[i].mod_hi, table.pay[i].mod_lo) < since);
+        const bool keep = i < n && !(row_mod(table[i]) < since);
         const unsigned long long b = __ballot(keep);
         const int before = __popcll(b & ((1ull << lane) - 1));
         if (lane == 0) s_wave[w] = __popcll(b);
@@ -619,13 +613,13 @@ __global__ void k_event_init(long long* __restrict__ event)
     if (threadIdx.x == 0) { event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
 }
 
-__global__ __launch_bounds__(256) void k_remap(Dec* __restrict__ dec, uint64_t n,
+__global__ __launch_bounds__(256) void k_remap(Row* __restrict__ table, uint64_t n,
                                                const uint32_t* __restrict__ lut, uint32_t nl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t r = dec[i].rank;
-    if (r < nl) dec[i].rank = lut[r];
+    const uint32_t r = table[i].rank;
+    if (r < nl) table[i].rank = lut[r];
 }
 
 // ============================================================ host-side context
@@ -665,10 +659,8 @@ struct crdt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t local_rank = 0;
-    Dec* dec = nullptr;
-    Pay* pay = nullptr;
+    Row* table = nullptr;
     uint64_t cap = 0;
-    Table table() const { return Table{dec, pay, cap}; }
     int64_t canonical = 0;
 
     Misc* d_misc = nullptr;
@@ -916,7 +908,7 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
         c->apply_total++;
         if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
         k_apply<<<grid_for(e - b, kApplyPerBlock), kApplyThreads, 0, c->stream>>>(
-            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table(), c->d_Rj.p, c->d_misc, dflags);
+            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
         if (timed) ev_record(c, ev_base + 2 + 2 * (size_t)j);
     }
     HIPCHK(hipGetLastError());
@@ -1018,8 +1010,7 @@ void crdt_destroy(crdt_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->dec) hipFree(c->dec);
-    if (c->pay) hipFree(c->pay);
+    if (c->table) hipFree(c->table);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
     c->d_M.release(); c->d_event.release(); c->d_offs.release(); c->d_tstart.release();
@@ -1037,25 +1028,18 @@ void crdt_destroy(crdt_ctx* c) {
 
 int crdt_reserve(crdt_ctx* c, uint64_t capacity) {
     if (!c) return CRDT_E_INVALID;
-    if (capacity <= c->cap && c->dec) return CRDT_OK;
+    if (capacity <= c->cap && c->table) return CRDT_OK;
     if (capacity > (1ull << 32)) return CRDT_E_INVALID;   // key ids are uint32
     HIPCHK(hipSetDevice(c->device));
     const uint64_t newcap = std::max<uint64_t>(capacity, 16);
-    Dec* d = nullptr;
-    Pay* p = nullptr;
-    HIPALLOC(hipMalloc(&d, newcap * sizeof(Dec)));
-    if (hipMalloc(&p, newcap * sizeof(Pay)) != hipSuccess) { hipFree(d); return CRDT_E_NOMEM; }
-    if (c->dec && c->cap) {
-        HIPCHK(hipMemcpyAsync(d, c->dec, c->cap * sizeof(Dec), hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(p, c->pay, c->cap * sizeof(Pay), hipMemcpyDeviceToDevice, c->stream));
-    }
-    HIPCHK(hipMemsetAsync(d + c->cap, 0x80, (newcap - c->cap) * sizeof(Dec), c->stream));
-    HIPCHK(hipMemsetAsync(p + c->cap, 0x80, (newcap - c->cap) * sizeof(Pay), c->stream));
+    Row* t = nullptr;
+    HIPALLOC(hipMalloc(&t, newcap * sizeof(Row)));
+    if (c->table && c->cap)
+        HIPCHK(hipMemcpyAsync(t, c->table, c->cap * sizeof(Row), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(t + c->cap, 0x80, (newcap - c->cap) * sizeof(Row), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->dec) hipFree(c->dec);
-    if (c->pay) hipFree(c->pay);
-    c->dec = d;
-    c->pay = p;
+    if (c->table) hipFree(c->table);
+    c->table = t;
     c->cap = newcap;
     return CRDT_OK;
 }
@@ -1099,7 +1083,7 @@ int crdt_put_rows(crdt_ctx* c, const uint32_t* key_id, const int64_t* lt, const 
     if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
     if ((st = stage(c, c->s_mod, mod, n, mem, &dm))) return st;
     if ((st = reset_misc(c))) return st;
-    k_put_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dl, dr, dv, dm, n, c->table(), c->d_misc);
+    k_put_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dl, dr, dv, dm, n, c->table, c->cap, c->d_misc);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1138,7 +1122,8 @@ int crdt_put_stamped(crdt_ctx* c, const uint32_t* key_id, const uint32_t* val, u
     if ((st = stage(c, c->s_key, key_id, n, mem, &dk))) return st;
     if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
     if ((st = reset_misc(c))) return st;
-    k_put_stamped<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dv, n, stamp, c->local_rank, c->table(), c->d_misc);
+    k_put_stamped<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dv, n, stamp, c->local_rank, c->table, c->cap,
+                                                           c->d_misc);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1172,7 +1157,7 @@ int crdt_read_rows(crdt_ctx* c, const uint32_t* key_id, uint64_t n, int64_t* lt,
         dv = val ? c->s_val.p : nullptr;
     }
     if ((st = reset_misc(c))) return st;
-    k_read_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, n, c->table(), dl, dr, dv, dm, c->d_misc);
+    k_read_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, n, c->table, c->cap, dl, dr, dv, dm, c->d_misc);
     HIPCHK(hipGetLastError());
     if (mem == CRDT_MEM_HOST) {
         if (lt) HIPCHK(hipMemcpyAsync(lt, dl, n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
@@ -1191,7 +1176,7 @@ int crdt_refresh_canonical(crdt_ctx* c, uint64_t n_rows, int64_t* out_lt) {
     k_fill_i64<<<1, 64, 0, c->stream>>>(c->d_word.p, 1, INT64_MIN);
     if (n_rows) {
         const unsigned g = std::min<unsigned>(grid_for(n_rows, 256), 2048);
-        k_refresh<<<g, 256, 0, c->stream>>>(c->dec, n_rows, c->d_word.p);
+        k_refresh<<<g, 256, 0, c->stream>>>(c->table, n_rows, c->d_word.p);
         HIPCHK(hipGetLastError());
     }
     long long w = 0;
@@ -1212,9 +1197,9 @@ int crdt_modified_since(crdt_ctx* c, uint64_t n_rows, int64_t since_lt, uint32_t
     const unsigned nb = grid_for(n_rows, kMsPerBlock);
     HIPALLOC(c->s_out.ensure(n_rows + nb));
     uint32_t* counts = c->s_out.p + n_rows;
-    k_ms_count<<<nb, 256, 0, c->stream>>>(c->table(), n_rows, since_lt, counts);
+    k_ms_count<<<nb, 256, 0, c->stream>>>(c->table, n_rows, since_lt, counts);
     k_ms_scan<<<1, 1024, 0, c->stream>>>(counts, nb, c->d_word.p);
-    k_ms_write<<<nb, 256, 0, c->stream>>>(c->table(), n_rows, since_lt, counts, c->s_out.p);
+    k_ms_write<<<nb, 256, 0, c->stream>>>(c->table, n_rows, since_lt, counts, c->s_out.p);
     HIPCHK(hipGetLastError());
     long long total = 0;
     HIPCHK(hipMemcpyAsync(&total, c->d_word.p, sizeof(total), hipMemcpyDeviceToHost, c->stream));
@@ -1228,8 +1213,7 @@ int crdt_clear_rows(crdt_ctx* c, uint64_t first, uint64_t count) {
     if (!c || first > c->cap || count > c->cap - first) return CRDT_E_INVALID;
     if (count == 0) return CRDT_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(c->dec + first, 0x80, count * sizeof(Dec), c->stream));
-    HIPCHK(hipMemsetAsync(c->pay + first, 0x80, count * sizeof(Pay), c->stream));
+    HIPCHK(hipMemsetAsync(c->table + first, 0x80, count * sizeof(Row), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
 }
@@ -1241,7 +1225,7 @@ int crdt_remap_ranks(crdt_ctx* c, uint64_t n_rows, const uint32_t* old_to_new, u
     const uint32_t* dl;
     int st;
     if ((st = stage(c, c->s_rank, old_to_new, n_ranks, CRDT_MEM_HOST, &dl))) return st;
-    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->dec, n_rows, dl, n_ranks);
+    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table, n_rows, dl, n_ranks);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
