@@ -10,10 +10,15 @@ Crdt.merge calls, crdt.dart:77-94) with every input already resident in HBM.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-N > 1: keys are sharded by key % N (strong scaling: the total stays 1B);
-changeset j is homed on rank j % N for the canonical-clock scan; the per-
-changeset maxima and the first-exception word are combined with RCCL
-all-reduces (torch.distributed "nccl" = RCCL over xGMI).
+N > 1, --scaling weak (default): the job is N x the single-GPU workload —
+N·1B records, keys over N·2^28 ids sharded key % N, N·2^27 local keys; every
+rank generates its own part (its 2^28 slots), changeset j is the rank-major
+concatenation of the ranks' parts of replica j.  Per changeset one all-gather
+of the part maxima (N x R int64) plus the MIN/MAX event reductions of
+crdt_amd/dist.py::sharded_merge_parts — no records cross xGMI.
+--scaling strong: the total stays 1B, keys sharded key % N, changeset j homed on
+rank j % N (dist.py::sharded_merge, three int64 all-reduces).
+Collectives are torch.distributed "nccl" = RCCL over xGMI.
 """
 from __future__ import annotations
 
@@ -48,6 +53,7 @@ def parse():
     p.add_argument("--local", type=int, default=1 << 27)
     p.add_argument("--zipf", type=float, default=0.8)
     p.add_argument("--order", choices=["shuffled", "ascending"], default="shuffled")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
@@ -64,12 +70,37 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # CRDT_BENCH_BACKEND=gloo: rehearsal of N ranks on one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("CRDT_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    from crdt_amd.dist import sharded_merge, sharded_merge_parts, torch_all_gather, torch_reducers
+    if world > 1:
+        red_max, red_min = torch_reducers(dist)
+        gather = torch_all_gather(dist)
     from crdt_amd import DeviceTable
     from crdt_amd.workload import gen_cfg2, gen_fanin
 
     t0 = time.time()
-    if args.config == "fanin":
+    weak = world > 1 and args.scaling == "weak"
+    if args.config == "fanin" and weak:
+        # this rank's part: a full single-GPU fan-in over its own 2^28 slots (global key = slot*N + rank)
+        wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                       device=dev, order=args.order, rank=0, world=1, seed=0xC0FFEE04 + 7919 * rank)
+        c0 = torch.tensor([wl["c0"]], dtype=torch.int64, device=dev)
+        red_max(c0)                                               # refreshCanonicalTime of the whole map
+        wl["c0"] = int(c0.item())
+        cnt = torch.from_numpy(np.diff(wl["owned_offsets"].astype(np.int64))).to(dev)
+        allc = gather(cnt).cpu().numpy()
+        wl["index_base"] = allc[:rank].sum(axis=0) if rank else np.zeros(allc.shape[1], np.int64)
+        wl["total"] = int(allc.sum())
+        workload = (f"fanin weak x{world}: {wl['total']:,} records = {wl['R']} replicas x "
+                    f"{world * wl['n_per_replica']:,}, per rank Zipf({args.zipf}) keys over its 2^"
+                    f"{int(np.log2(args.keys))} slots of {world}·2^{int(np.log2(args.keys))} ids (key % N), "
+                    f"{args.order} order, local map {world}·2^{int(np.log2(args.local))} keys")
+    elif args.config == "fanin":
         wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
                        device=dev, order=args.order, rank=rank, world=world)
         workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
@@ -98,14 +129,14 @@ def main():
         table.canonical = wl["c0"]
         torch.cuda.synchronize()
 
-    from crdt_amd.dist import sharded_merge, torch_reducers
-    if world > 1:
-        red_max, red_min = torch_reducers(dist)
-
     def step(flags=None):
         if world == 1:
             res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
             return res
+        if weak:
+            # per changeset: part scan -> all-gather maxima -> clock -> MIN(event) -> resolve -> MAX -> apply
+            return sharded_merge_parts(table, own_cols, wl["wall"], wl["index_base"], d_max, d_ev, gather,
+                                       red_max, red_min, rank, win_flags=flags)
         # key-sharded: home scan -> MAX(M_j) -> clock -> MIN(event) -> resolve -> MAX(details) -> apply
         return sharded_merge(table, home_cols, own_cols, wl["wall"], d_max, d_ev, red_max, red_min,
                              win_flags=flags)
@@ -129,9 +160,9 @@ def main():
         barrier()
         dt = time.perf_counter() - ts
         if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+            t = torch.tensor([int(dt * 1e9)], device=dev, dtype=torch.int64)
+            red_max(t)                                            # max over ranks (ns)
+            dt = float(t.item()) / 1e9
         step_ms.append(dt * 1e3)
         tm = table.timing()
         apply_ms += tm["apply_ms"]
@@ -193,9 +224,9 @@ def main():
         "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
         "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "scaling": "weak" if (world == 1 or weak) else "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
         "config": {"workload": workload, "records": total_records, "replicas": R,
-                   "parallelism": f"keyshard{world}" if world > 1 else "single",
+                   "parallelism": (f"keyshard{world}-{'parts' if weak else 'home'}" if world > 1 else "single"),
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),

@@ -81,7 +81,7 @@ SIGNATURES = {
     "crdt_refresh_canonical": (_INT, [_P, _U64, _P]),
     "crdt_merge": (_INT, [_P, _P, _I64, _P, _P]),
     "crdt_merge_scan": (_INT, [_P, _P, _I64, _P]),
-    "crdt_merge_clock": (_INT, [_P, _P, _I64, _P, _P]),
+    "crdt_merge_clock": (_INT, [_P, _P, _I64, _P, _P, _P, _P]),
     "crdt_merge_resolve": (_INT, [_P, _P, _P]),
     "crdt_merge_apply": (_INT, [_P, _P, _I64, _P, _P, _P]),
     "crdt_set_timing": (_INT, [_P, _INT]),

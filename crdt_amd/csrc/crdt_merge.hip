@@ -262,8 +262,12 @@ __global__ __launch_bounds__(64) void k_verify(
     const Misc* __restrict__ misc, const uint32_t* __restrict__ cand_tile,
     long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
     uint32_t* __restrict__ cand_kind, int64_t* __restrict__ cand_ms,
+    const long long* __restrict__ pbase, const unsigned long long* __restrict__ ibase,
     long long* __restrict__ event)
 {
+    // pbase / ibase (optional): this ctx holds only a PART of changeset j, preceded in
+    // its iteration order by records of other ranks whose max lt is pbase[j] and whose
+    // count is ibase[j] (key-sharded "parts" protocol, crdt_amd/dist.py).
     const int lane = threadIdx.x;
     const uint32_t n = misc->cand_count;
     for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
@@ -276,6 +280,7 @@ __global__ __launch_bounds__(64) void k_verify(
         const uint32_t j = lo;
         const uint32_t t = gt - tstart[j];
         int64_t P = Cprev[j];
+        if (pbase) P = imax(P, (int64_t)pbase[j]);
         for (uint32_t u = tstart[j] + lane; u < gt; u += 64) P = imax(P, T[u]);
         P = wave_max(P);
         const uint64_t base = offs[j] + (uint64_t)t * kTile;
@@ -311,7 +316,8 @@ __global__ __launch_bounds__(64) void k_verify(
         }
         if (lane == 0) {
             if (found) {
-                const long long key = (long long)(((int64_t)j << kLowBits) | (int64_t)(fi - offs[j]));
+                const int64_t idx = (int64_t)(fi - offs[j]) + (ibase ? (int64_t)ibase[j] : 0);
+                const long long key = (long long)(((int64_t)j << kLowBits) | idx);
                 cand_key[c] = key;
                 cand_P[c] = fp;
                 cand_kind[c] = fkind;
@@ -680,6 +686,8 @@ struct crdt_ctx {
     DBuf<uint8_t> s_flags;
     DBuf<uint32_t> s_out;
     DBuf<long long> d_word;
+    DBuf<unsigned long long> d_ibase;
+    HBuf<uint64_t> h_ibase;
     // per-call plan (set by scan, used by later phases)
     uint32_t plan_R = 0;
     uint64_t plan_tiles = 0;
@@ -847,7 +855,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
 }
 
 int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long long* d_maxima,
-                long long* d_event) {
+                long long* d_event, const long long* d_pbase = nullptr, const uint64_t* h_ibase = nullptr) {
     const uint32_t R = c->plan_R;
     if (!home || home->n_changesets != R) return CRDT_E_INVALID;
     int st;
@@ -856,6 +864,14 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
     HIPALLOC(c->d_Cprev.ensure(R + 1));
     HIPALLOC(c->d_Rj.ensure(R + 1));
     HIPALLOC(c->d_Cj.ensure(R + 1));
+    const unsigned long long* d_ibase = nullptr;
+    if (h_ibase && R) {
+        HIPALLOC(c->d_ibase.ensure(R));
+        HIPALLOC(c->h_ibase.ensure(R));
+        memcpy(c->h_ibase.p, h_ibase, R * sizeof(uint64_t));
+        HIPCHK(hipMemcpyAsync(c->d_ibase.p, c->h_ibase.p, R * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        d_ibase = c->d_ibase.p;
+    }
     k_event_init<<<1, 64, 0, c->stream>>>(d_event);
     if (R) k_clock<<<1, 1024, 0, c->stream>>>(d_maxima, R, wall, c->canonical, c->d_Cprev.p, c->d_Rj.p,
                                               c->d_Cj.p, d_event);
@@ -863,7 +879,7 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
         k_verify<<<kVerifyBlocks, 64, 0, c->stream>>>(
             cols.lt, cols.rank, cols.millis, c->d_offs.p, c->d_tstart.p, R, c->d_T.p, c->d_Cprev.p, wall,
             c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
-            c->d_candms.p, d_event);
+            c->d_candms.p, d_pbase, d_ibase, d_event);
     HIPCHK(hipGetLastError());
     return CRDT_OK;
 }
@@ -1021,6 +1037,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->s_key.release(); c->s_rank.release(); c->s_val.release(); c->s_lt.release();
     c->s_millis.release(); c->s_mod.release(); c->s_flags.release(); c->s_out.release();
     c->d_word.release();
+    c->d_ibase.release();
+    c->h_ibase.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -1290,11 +1308,12 @@ int crdt_merge_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, uint64_t*
 }
 
 int crdt_merge_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const uint64_t* d_maxima,
-                     uint64_t* d_event) {
+                     const int64_t* d_prefix_max, const uint64_t* index_base, uint64_t* d_event) {
     if (!c || !d_maxima || !d_event) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
     int st = phase_clock(c, home, wall, reinterpret_cast<const long long*>(d_maxima),
-                         reinterpret_cast<long long*>(d_event));
+                         reinterpret_cast<long long*>(d_event), reinterpret_cast<const long long*>(d_prefix_max),
+                         index_base);
     if (st) return st;
     HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_event[0] next
     return CRDT_OK;

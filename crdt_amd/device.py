@@ -216,11 +216,14 @@ class DeviceTable:
         self._check(self._lib.crdt_merge_scan(self._ctx, ctypes.byref(b), int(wall),
                                               ctypes.c_void_p(d_maxima.data_ptr())), "crdt_merge_scan")
 
-    def merge_clock(self, home, wall: int, d_maxima, d_event):
+    def merge_clock(self, home, wall: int, d_maxima, d_event, d_prefix_max=None, index_base=None):
         b, c, _ = self._batch(*home)
-        self._check(self._lib.crdt_merge_clock(self._ctx, ctypes.byref(b), int(wall),
-                                               ctypes.c_void_p(d_maxima.data_ptr()),
-                                               ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_clock")
+        ib = None if index_base is None else np.ascontiguousarray(index_base, dtype=np.uint64)
+        self._check(self._lib.crdt_merge_clock(
+            self._ctx, ctypes.byref(b), int(wall), ctypes.c_void_p(d_maxima.data_ptr()),
+            None if d_prefix_max is None else ctypes.c_void_p(d_prefix_max.data_ptr()),
+            None if ib is None else ib.ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_clock")
 
     def merge_resolve(self, home, d_event):
         b, c, _ = self._batch(*home)

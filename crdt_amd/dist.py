@@ -36,6 +36,56 @@ def sharded_merge(table, home, owned, wall: int, d_maxima, d_event, all_reduce_m
     return table.merge_apply(owned, wall, d_event, win_flags=win_flags)
 
 
+def sharded_merge_parts(table, part, wall: int, index_base, d_maxima, d_event, all_gather, all_reduce_max,
+                        all_reduce_min, rank: int, win_flags=None) -> dict:
+    """Batched merge when changeset j is the concatenation, in rank order, of the parts
+    the ranks own (weak-scaling layout: every rank generates / ingests its own part).
+
+    ``index_base[j]`` = records of changeset j held by lower ranks (host, from one
+    all-gather of the per-rank counts).  Collectives: all-gather of the R per-part maxima
+    (the global M_j is their max; the exception scan of this part starts from the max
+    of the lower ranks' parts), then the same MIN / MAX event reductions as
+    ``sharded_merge``.
+    """
+    import torch
+    table.merge_scan(part, wall, d_maxima)
+    g = all_gather(d_maxima)                                     # [G, R]
+    prefix = torch.full_like(d_maxima, torch.iinfo(torch.int64).min)
+    if rank > 0:
+        prefix.copy_(g[:rank].max(dim=0).values)
+    d_maxima.copy_(g.max(dim=0).values)
+    if d_maxima.is_cuda:                     # torch's stream -> the library's stream
+        torch.cuda.synchronize()
+    table.merge_clock(part, wall, d_maxima, d_event, d_prefix_max=prefix, index_base=index_base)
+    all_reduce_min(d_event[:1])
+    table.merge_resolve(part, d_event)
+    all_reduce_max(d_event[1:])
+    return table.merge_apply(part, wall, d_event, win_flags=win_flags)
+
+
+def torch_all_gather(dist):
+    """all-gather of an int64 vector into a [G, n] tensor (host-staged on gloo)."""
+    import torch
+    host_staged = dist.get_backend() == "gloo"
+
+    def _gather(t):
+        world = dist.get_world_size()
+        if not host_staged:
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t.contiguous())
+            return out.view(world, -1)
+        src = t.cpu() if t.is_cuda else t
+        out = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(out, src)
+        g = torch.stack(out)
+        if t.is_cuda:
+            g = g.to(t.device)
+            torch.cuda.synchronize()
+        return g
+
+    return _gather
+
+
 def torch_reducers(dist):
     """all-reduce helpers over torch.distributed (``nccl`` = RCCL on ROCm, or ``gloo``)."""
     import torch

@@ -163,10 +163,17 @@ int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint
  *                  INT64_MAX: none), then MAX all-reduce of d_event[1..3] after resolve
  *                  (canonical at the failure, kind, Hlc.millis of the failing record)
  * then applies the records it owns (any rank: owned batch, same n_changesets).
- * scan and clock synchronise the ctx stream before returning. */
+ * scan and clock synchronise the ctx stream before returning.
+ *
+ * "Parts" protocol (changeset j = the concatenation, in rank order, of the parts
+ * the ranks own): every rank scans its own part; the host all-gathers the R maxima,
+ * passes the global max in d_maxima, the max of the lower ranks' parts in
+ * d_prefix_max (device, [R]) and their record counts in index_base (host, [R]).
+ * The home protocol passes NULL for both. */
 int crdt_merge_scan(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis, uint64_t* d_maxima);
 int crdt_merge_clock(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis,
-                     const uint64_t* d_maxima, uint64_t* d_event);
+                     const uint64_t* d_maxima, const int64_t* d_prefix_max, const uint64_t* index_base,
+                     uint64_t* d_event);
 int crdt_merge_resolve(crdt_ctx* ctx, const crdt_batch* home, uint64_t* d_event);
 int crdt_merge_apply(crdt_ctx* ctx, const crdt_batch* owned, int64_t wall_millis,
                      const uint64_t* d_event, uint8_t* win_flags, crdt_result* out);

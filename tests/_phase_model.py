@@ -51,7 +51,7 @@ class PhaseModel:
             d_max[j] = int(seg.max()) if len(seg) else I64MIN
 
     # K3b + K3c
-    def merge_clock(self, home, wall, d_max, d_ev):
+    def merge_clock(self, home, wall, d_max, d_ev, d_prefix_max=None, index_base=None):
         _, lt, rank, _, offs, millis = home
         offs = np.asarray(offs, np.int64)
         R = len(offs) - 1
@@ -72,12 +72,15 @@ class PhaseModel:
         self.cands = {}
         for j in range(R):                       # home changesets only have records here
             p = self.Cprev[j]
+            if d_prefix_max is not None:
+                p = max(p, int(d_prefix_max[j]))
+            ib = 0 if index_base is None else int(index_base[j])
             for x in range(offs[j], offs[j + 1]):
                 v = int(lt[x])
                 ms = int(millis[x]) if millis is not None else v >> SHIFT
                 dup = int(rank[x]) == self.local_rank
                 if (dup or ms - wall > DRIFT) and v > p:
-                    key = (j << 40) | (x - offs[j])
+                    key = (j << 40) | (x - offs[j] + ib)
                     self.cands[key] = (p, 2 if dup else 1, ms)
                     ev = min(ev, key)
                     break

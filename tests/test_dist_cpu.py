@@ -123,3 +123,88 @@ def test_route_by_owner_is_stable():
     routes = route_by_owner(key, np.array([0, 3, 6], np.uint64), 2)
     assert routes[0][0].tolist() == [1, 3, 5] and routes[0][1].tolist() == [0, 1, 3]
     assert routes[1][0].tolist() == [0, 2, 4] and routes[1][1].tolist() == [0, 2, 3]
+
+
+# ---------------------------------------------------------------- "parts" protocol
+def _parts_case(kw, world):
+    """One global case; changeset j's iteration order is rank-major (rank r's owned records first
+    for r = 0, then 1, ...).  Returns the reordered global case and each rank's part."""
+    case = make_case(**kw)
+    key, offs = case["key"], case["offsets"].astype(np.int64)
+    order = []
+    for j in range(len(offs) - 1):
+        seg = np.arange(offs[j], offs[j + 1])
+        for r in range(world):
+            order.extend(seg[key[seg] % world == r])
+    order = np.array(order, dtype=np.int64)
+    g = dict(case)
+    for f in ("key", "lt", "rank", "val"):
+        g[f] = case[f][order]
+    if case["millis"] is not None:
+        g["millis"] = case["millis"][order]
+    return g
+
+
+def _parts_worker(rank, world, port, case_kw, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from crdt_amd.dist import sharded_merge_parts, torch_all_gather
+        case = _parts_case(case_kw, world)
+        cap = -(-case["n_ids"] // world)
+        t = PhaseModel(cap, case["local_rank"], case["c0"])
+        loc = case["local"]
+        ids = np.arange(case["n_local"])
+        mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
+        t.put_rows(ids[mine] // world, loc["lt"][mine], loc["rank"][mine], loc["val"][mine], loc["mod"][mine])
+        routes = route_by_owner(case["key"], case["offsets"], world)
+        idx, offs_r = routes[rank]
+        millis = None if case["millis"] is None else case["millis"][idx]
+        part = ((case["key"][idx] // world).astype(np.uint32), case["lt"][idx], case["rank"][idx],
+                case["val"][idx], offs_r, millis)
+        counts = np.stack([np.diff(routes[r][1].astype(np.int64)) for r in range(world)])
+        ibase = counts[:rank].sum(axis=0) if rank else np.zeros(counts.shape[1], np.int64)
+        R = len(case["offsets"]) - 1
+        d_max = torch.zeros(max(R, 1), dtype=torch.int64)
+        d_ev = torch.zeros(4, dtype=torch.int64)
+        flags = np.zeros(len(idx), np.uint8)
+        red_max, red_min = torch_reducers(dist)
+        res = sharded_merge_parts(t, part, case["wall"], ibase, d_max, d_ev, torch_all_gather(dist), red_max,
+                                  red_min, rank, win_flags=flags)
+        q.put((rank, res, t.lt, t.rank, t.val, t.mod, idx, flags))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["r4_ties", "dup_node", "drift", "drift_late", "send_overflow",
+                                  "explicit_millis", "dup_and_drift"])
+def test_parts_protocol_equals_single_table(name):
+    kw = dict(CASE_SPECS)[name]
+    world = 2
+    case = _parts_case(kw, world)
+    orows, ores, oflags = oracle_run(case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_parts_worker, args=(r, world, port, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    flags = np.zeros(len(case["key"]), np.uint8)
+    tot = [0, 0]
+    for rank, res, lt, rk, val, mod, idx, fl in outs:
+        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
+            assert res[f] == ores[f], (name, rank, f, res[f], ores[f])
+        tot[0] += res["n_present"]
+        tot[1] += res["n_won"]
+        flags[idx] = fl
+        keys = np.arange(case["n_ids"])
+        mine = keys % world == rank
+        slots = keys[mine] // world
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a[slots], orows[f][mine]), f
+    assert tot == [ores["n_present"], ores["n_won"]]
+    assert np.array_equal(flags, oflags)

@@ -152,19 +152,19 @@ def test_reserve_preserves_rows(gpu_device):
     assert (lt[0], rank[0], val[0], mod[0]) == (42, 1, 7, 43) and mod[1] < 0
 
 
-def _sharded_gpu_worker(rank, world, port, case_kw, q):
+def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home"):
     import os
 
     import torch
     import torch.distributed as dist
 
     from crdt_amd import DeviceTable
-    from crdt_amd.dist import sharded_merge, torch_reducers
-    from tests.test_dist_cpu import _split
+    from crdt_amd.dist import route_by_owner, sharded_merge, sharded_merge_parts, torch_all_gather, torch_reducers
+    from tests.test_dist_cpu import _parts_case, _split
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        case = make_case(**case_kw)
+        case = make_case(**case_kw) if protocol == "home" else _parts_case(case_kw, world)
         cap = -(-case["n_ids"] // world)
         t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
         loc = case["local"]
@@ -183,7 +183,15 @@ def _sharded_gpu_worker(rank, world, port, case_kw, q):
         d_ev = torch.zeros(4, dtype=torch.int64, device="cuda")
         flags = torch.zeros(max(len(idx), 1), dtype=torch.uint8, device="cuda")
         red_max, red_min = torch_reducers(dist)
-        res = sharded_merge(t, home_d, owned_d, case["wall"], d_max, d_ev, red_max, red_min, win_flags=flags)
+        if protocol == "home":
+            res = sharded_merge(t, home_d, owned_d, case["wall"], d_max, d_ev, red_max, red_min, win_flags=flags)
+        else:
+            routes = route_by_owner(case["key"], case["offsets"], world)
+            counts = np.stack([np.diff(routes[r][1].astype(np.int64)) for r in range(world)])
+            ibase = counts[:rank].sum(axis=0)
+            part = owned_d[:5] + (None if case["millis"] is None else dev(case["millis"][idx]),)
+            res = sharded_merge_parts(t, part, case["wall"], ibase, d_max, d_ev, torch_all_gather(dist), red_max,
+                                      red_min, rank, win_flags=flags)
         lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
         q.put((rank, res, lt, rk, val, mod, idx, flags[:len(idx)].cpu().numpy()))
         t.close()
@@ -191,19 +199,20 @@ def _sharded_gpu_worker(rank, world, port, case_kw, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("protocol", ["home", "parts"])
 @pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
-def test_two_rank_sharded_on_device(gpu_device, name):
-    """The device phase API under the multi-rank protocol (2 processes on one GPU, gloo)."""
+def test_two_rank_sharded_on_device(gpu_device, name, protocol):
+    """The device phase API under the multi-rank protocols (2 processes on one GPU, gloo)."""
     import torch.multiprocessing as mp
 
-    from tests.test_dist_cpu import _free_port
+    from tests.test_dist_cpu import _free_port, _parts_case
     kw = dict(CASE_SPECS)[name]
-    case = make_case(**kw)
+    case = make_case(**kw) if protocol == "home" else _parts_case(kw, 2)
     orows, ores, oflags = oracle_run(case)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_gpu_worker, args=(r, 2, port, kw, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_gpu_worker, args=(r, 2, port, kw, q, protocol)) for r in range(2)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=180) for _ in range(2)]
