@@ -1301,8 +1301,11 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
 int crdt_merge_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, uint64_t* d_maxima) {
     if (!c || !d_maxima) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
+    if (c->timing && home) HIPCHK(ensure_events(c, 4 + 2 * (size_t)home->n_changesets + 1));
+    ev_record(c, 0);
     int st = phase_scan(c, home, wall, reinterpret_cast<long long*>(d_maxima));
     if (st) return st;
+    ev_record(c, 1);
     HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_maxima next
     return CRDT_OK;
 }
@@ -1332,10 +1335,17 @@ int crdt_merge_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const u
                      uint8_t* win_flags, crdt_result* out) {
     if (!c || !d_event) return CRDT_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    const bool timing = c->timing;
-    c->timing = false;
-    int st = phase_apply(c, owned, wall, reinterpret_cast<const long long*>(d_event), win_flags, out, 0);
-    c->timing = timing;
+    // timing (when enabled): scan_ms = the scan call, clock_ms = scan end -> apply start (clock, verify,
+    // resolve and the host collectives between the calls), apply launches sampled as in crdt_merge
+    const uint32_t R = c->plan_R;
+    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
+    ev_record(c, 2);
+    int st = phase_apply(c, owned, wall, reinterpret_cast<const long long*>(d_event), win_flags, out, 3);
+    if (c->timing) {
+        ev_record(c, 3 + 2 * (size_t)R + 1);
+        hipStreamSynchronize(c->stream);
+    }
+    collect_timing(c, R, true);
     return st;
 }
 
