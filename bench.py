@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", choices=["fanin", "cfg2"], default="fanin")
+    p.add_argument("--config", choices=["fanin", "cfg2", "cfg3", "cfg5"], default="fanin")
     p.add_argument("--records", type=int, default=1_000_000_000)
     p.add_argument("--replicas", type=int, default=1024)
     p.add_argument("--keys", type=int, default=1 << 28)
@@ -82,7 +82,7 @@ def main():
         red_max, red_min = torch_reducers(dist)
         gather = torch_all_gather(dist)
     from crdt_amd import DeviceTable
-    from crdt_amd.workload import gen_cfg2, gen_fanin
+    from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
 
     t0 = time.time()
     weak = world > 1 and args.scaling == "weak"
@@ -107,10 +107,20 @@ def main():
         workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
                     f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
                     f"{args.order} order), local map 2^{int(np.log2(args.local))} keys, keys sharded key%N")
-    else:
+    elif args.config == "cfg2":
         assert world == 1, "cfg2 is a single-GPU configuration"
         wl = gen_cfg2(device=dev)
         workload = "cfg2: 10M-key local map + one 10M-record changeset, ~50% key overlap"
+    elif args.config == "cfg3":
+        assert world == 1, "cfg3 is a single-GPU configuration"
+        wl = gen_cfg3(device=dev)
+        workload = ("cfg3: 100M-key local map, 1024 replicas x 97,657 records, Zipf(1.0) keys, millis over 8 "
+                    "values x counters over 4 (ties decided by node rank)")
+    else:
+        assert world == 1, "cfg5 runs on one GPU here"
+        wl = gen_cfg5(device=dev)
+        workload = ("cfg5 streaming: 100M-key table, 100 deltas x 10M records, one merge call per delta "
+                    "(advancing wall), 10% tombstones, peers 1..16")
     torch.cuda.synchronize()
     log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
 
@@ -131,6 +141,24 @@ def main():
         torch.cuda.synchronize()
 
     def step(flags=None):
+        if wl.get("per_call"):                       # streaming: one crdt_merge per delta
+            offs, tot = wl["owned_offsets"], None
+            for d in range(wl["R"]):
+                b, e = int(offs[d]), int(offs[d + 1])
+                fl = False if flags is None else flags[b:e]
+                r, _ = table.merge(own["key"][b:e], own["lt"][b:e], own["rank"][b:e], own["val"][b:e],
+                                   np.array([0, e - b], np.uint64), int(wl["walls"][d]), win_flags=fl)
+                if table_timing[0]:
+                    table_timing[1].append(table.timing())
+                if tot is None:
+                    tot = dict(r)
+                else:
+                    tot.update({k: r[k] for k in ("status", "canonical_lt", "exc_index", "drift_ms", "counter")})
+                    tot["n_present"] += r["n_present"]
+                    tot["n_won"] += r["n_won"]
+                if r["status"] != 0:
+                    break
+            return tot
         if world == 1:
             res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
             return res
@@ -147,10 +175,12 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    table_timing = [False, []]                     # per-call timing records (streaming config)
     for _ in range(args.warmup):
         reset()
         step()
     table.set_timing(True)
+    table_timing[0] = True
     step_ms, apply_ms, apply_launches, apply_total, scan_ms, clock_ms, dev_ms = [], 0.0, 0, 0, 0.0, 0.0, 0.0
     res = None
     for _ in range(args.steps):
@@ -165,7 +195,8 @@ def main():
             red_max(t)                                            # max over ranks (ns)
             dt = float(t.item()) / 1e9
         step_ms.append(dt * 1e3)
-        tm = table.timing()
+        tms, table_timing[1] = table_timing[1] or [table.timing()], []
+        tm = {k: sum(t[k] for t in tms) for k in tms[0]}
         apply_ms += tm["apply_ms"]
         apply_launches += tm["apply_launches"]
         apply_total += tm["apply_total"]
@@ -173,6 +204,7 @@ def main():
         clock_ms += tm["clock_ms"]
         dev_ms += tm["total_ms"]
     table.set_timing(False)
+    table_timing[0] = False
     assert res["status"] == 0, res
     ms_per_step = float(np.mean(step_ms))
     total_records = wl["total"]
@@ -204,17 +236,20 @@ def main():
         reset()
         flags = torch.zeros(max(n_owned, 1), dtype=torch.uint8, device=dev)
         r2 = step(flags=flags) if world == 1 else None
-        keys = own["key"]
-        won_keys = torch.unique(keys[flags[:n_owned].bool()])
-        all_keys = torch.unique(keys)
-        u_touch = int((all_keys < wl["n_local_rows"]).sum().item()) if args.config == "fanin" else \
-            int((all_keys < wl["n_local"]).sum().item())
-        u_win = int(won_keys.numel())
+        if wl.get("per_call"):      # every call is its own merge: U counted per call (= its records)
+            u_touch, u_win = int(r2["n_present"]), int(r2["n_won"])
+        else:
+            keys = own["key"]
+            all_keys = torch.unique(keys)
+            u_touch = int((all_keys < wl["n_local_rows"]).sum().item()) if args.config in ("fanin", "cfg3") \
+                else int((all_keys < wl["n_local"]).sum().item())
+            del all_keys
+            u_win = int(torch.unique(keys[flags[:n_owned].bool()]).numel())
         b_alg = 20 * total_records + 12 * u_touch + 24 * u_win
         job = {"U_touch": u_touch, "U_win": u_win, "B_alg_bytes": b_alg,
                "hbm_frac_job": round(b_alg / (ms_per_step / 1e3) / HBM_PEAK, 4),
                "records_won_total": int(r2["n_won"])}
-        del flags, won_keys, all_keys
+        del flags
 
     # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
     cpu = None
@@ -263,7 +298,8 @@ def cpu_baseline(wl, budget_s):
         cols = [own[k][sl].cpu().numpy() for k in ("key", "lt", "rank", "val")]
         ts = time.perf_counter()
         res, _ = t.merge(cols[0].astype(np.uint32), cols[1], cols[2].astype(np.uint32),
-                         cols[3].astype(np.uint32), np.array([0, e - b], np.uint64), wl["wall"], faithful=True,
+                         cols[3].astype(np.uint32), np.array([0, e - b], np.uint64),
+                         int(wl["walls"][done]) if wl.get("per_call") else wl["wall"], faithful=True,
                          want_flags=False)
         el += time.perf_counter() - ts
         done += 1

@@ -11,6 +11,14 @@ canonical-clock scan).
 
 cfg2 (configs[1]): one 10M-record changeset against a 10M-key table, ~50%
 overlap (5M existing ids + 5M new ids).
+
+cfg3 (configs[2]): the fan-in generator at 100M keys / 100M records / 1024
+replicas, Zipf(1.0), millis over 8 values and counters over 4 (heavy
+(millis, counter) ties, decided by the node rank).
+
+cfg5 (configs[4]): streaming — a 100M-key table, 100 deltas of 10M records,
+one merge call per delta (advancing wall clock), 10% tombstones, optional
+drift / duplicate-node injection at (delta 37, position 4,999,999).
 """
 from __future__ import annotations
 
@@ -152,3 +160,78 @@ def gen_cfg2(n_local: int = 10_000_000, n_remote: int = 10_000_000, overlap: flo
             "c0": int(l_lt.max().item()), "wall": BASE_MILLIS + millis_span + 1000, "R": 1,
             "n_per_replica": n_remote, "total": n_remote, "K": n_local + n_new, "n_local": n_local,
             "world": 1, "rank": 0}
+
+
+def gen_cfg3(device="cuda", total: int = 100_000_000, K: int = 100_000_000, R: int = 1024) -> dict:
+    """configs[2]: SURVEY §8(d) cfg3 (seed 0xC0FFEE03)."""
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K, s=1.0, seed=0xC0FFEE03, device=device,
+                   millis_span=8, counter_span=4)
+    return wl
+
+
+def _affine(K: int, gen: torch.Generator, dev) -> tuple[int, int]:
+    """(a, b) with gcd(a, K) = 1: i -> (a*i + b) mod K is a bijection of [0, K)."""
+    while True:
+        a = int(torch.randint(1, K, (1,), device=dev, generator=gen).item()) | 1
+        if np.gcd(a, K) == 1:
+            return a, int(torch.randint(0, K, (1,), device=dev, generator=gen).item())
+
+
+def gen_cfg5(device="cuda", K: int = 100_000_000, n_delta: int = 10_000_000, deltas: int = 100,
+             tomb: float = 0.1, inject: str | None = None, inject_at: tuple[int, int] = (37, 4_999_999),
+             seed: int = 0xC0FFEE05, peers: int = 16, step_ms: int = 1000) -> dict:
+    """configs[4]: ``deltas`` merge calls of ``n_delta`` records each against a K-key table.
+
+    Delta d comes from peer ``1 + d % peers`` (local node rank 0), keys = an affine bijection of
+    [0, K) restricted to the first n_delta points (unique within the delta), millis in
+    [base + d*step_ms, base + (d+1)*step_ms), wall_d = base + (d+1)*step_ms + 500.
+    ``inject``: None, "drift" (millis = wall + 60_001) or "dup" (local rank, newest lt) at
+    ``inject_at`` = (delta, position)."""
+    assert n_delta <= K
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    n = n_delta * deltas
+    key = torch.empty(n, dtype=torch.int32, device=dev)
+    lt = torch.empty(n, dtype=torch.int64, device=dev)
+    rank = torch.empty(n, dtype=torch.int32, device=dev)
+    val = torch.empty(n, dtype=torch.int32, device=dev)
+    walls = np.zeros(deltas, np.int64)
+    aff = []
+    i = torch.arange(n_delta, device=dev, dtype=torch.int64)
+    for d in range(deltas):
+        a, b = _affine(K, gen, dev)
+        aff.append((a, b))
+        sl = slice(d * n_delta, (d + 1) * n_delta)
+        key[sl] = ((i * a + b) % K).to(torch.int32)
+        ms = BASE_MILLIS + d * step_ms + torch.randint(0, step_ms, (n_delta,), device=dev, generator=gen)
+        lt[sl] = (ms << 16) + torch.randint(0, 16, (n_delta,), device=dev, generator=gen)
+        rank[sl] = 1 + d % peers
+        v = (d * n_delta + i + 1).to(torch.int32)
+        v[torch.rand(n_delta, device=dev, generator=gen) < tomb] = -1          # NULL handle 0xFFFFFFFF
+        val[sl] = v
+        walls[d] = BASE_MILLIS + (d + 1) * step_ms + 500
+    if inject:
+        dj, pi = inject_at
+        x = dj * n_delta + pi
+        if inject == "drift":
+            lt[x] = (walls[dj] + 60_001) << 16
+        elif inject == "dup":
+            lt[x] = (walls[dj] + 1) << 16
+            rank[x] = 0
+        else:
+            raise ValueError(inject)
+    lgen = torch.Generator(device=dev)
+    lgen.manual_seed(seed ^ 0x5EED)
+    l_ms = BASE_MILLIS + torch.randint(0, deltas * step_ms, (K,), device=dev, generator=lgen)
+    l_lt = (l_ms << 16) + torch.randint(0, 16, (K,), device=dev, generator=lgen)
+    del l_ms
+    local = {"slot": torch.arange(K, device=dev, dtype=torch.int32), "lt": l_lt,
+             "rank": torch.zeros(K, device=dev, dtype=torch.int32),
+             "val": torch.arange(K, device=dev, dtype=torch.int32), "mod": l_lt.clone()}
+    offs = (np.arange(deltas + 1, dtype=np.uint64) * n_delta)
+    return {"owned": {"key": key, "lt": lt, "rank": rank, "val": val}, "owned_offsets": offs,
+            "home": {"lt": lt, "rank": rank}, "home_offsets": offs, "local": local, "n_local_rows": K,
+            "capacity": K, "c0": int(l_lt.max().item()), "wall": int(walls[0]), "walls": walls,
+            "per_call": True, "affine": aff, "R": deltas, "n_per_replica": n_delta, "total": n, "K": K,
+            "n_local": K, "world": 1, "rank": 0}

@@ -163,3 +163,24 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), f
+
+
+def test_workload_generators_cpu():
+    """Invariants of the BASELINE.json generators (run on CPU torch at small sizes)."""
+    import torch
+    from crdt_amd.workload import gen_cfg3, gen_cfg5
+    wl = gen_cfg5(device="cpu", K=10_007, n_delta=1000, deltas=6, inject="drift", inject_at=(3, 499))
+    own, offs = wl["owned"], wl["owned_offsets"]
+    for d in range(6):
+        k = own["key"][int(offs[d]):int(offs[d + 1])]
+        assert torch.unique(k).numel() == k.numel() and int(k.min()) >= 0 and int(k.max()) < 10_007
+    assert np.all(np.diff(wl["walls"]) > 0)
+    frac = float((own["val"] == -1).double().mean())
+    assert 0.07 < frac < 0.13
+    assert int(own["lt"][3 * 1000 + 499]) >> 16 == int(wl["walls"][3]) + 60_001
+    wl3 = gen_cfg3(device="cpu", total=20_000, K=50_000, R=16)
+    assert torch.unique(wl3["owned"]["lt"]).numel() <= 32
+    o3 = wl3["owned_offsets"]
+    for j in range(16):
+        k = wl3["owned"]["key"][int(o3[j]):int(o3[j + 1])]
+        assert torch.unique(k).numel() == k.numel()
