@@ -223,7 +223,11 @@ def gen_cfg5(device="cuda", K: int = 100_000_000, n_delta: int = 10_000_000, del
             raise ValueError(inject)
     lgen = torch.Generator(device=dev)
     lgen.manual_seed(seed ^ 0x5EED)
-    l_ms = BASE_MILLIS + torch.randint(0, deltas * step_ms, (K,), device=dev, generator=lgen)
+    # local rows: clocks over [base - span/2, base + 0.3 span) — the early deltas compete with them,
+    # and the canonical is below delta 37's wall clock, so the injected record is a recv() advance
+    span = deltas * step_ms
+    l_ms = BASE_MILLIS - span // 2 + torch.randint(0, span // 2 + (3 * span) // 10, (K,), device=dev,
+                                                   generator=lgen)
     l_lt = (l_ms << 16) + torch.randint(0, 16, (K,), device=dev, generator=lgen)
     del l_ms
     local = {"slot": torch.arange(K, device=dev, dtype=torch.int32), "lt": l_lt,
