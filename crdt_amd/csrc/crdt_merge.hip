@@ -38,8 +38,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kTile = kScanThreads * kScanItems; // 4096 records per scan tile
 constexpr int kApplyThreads = 256;
-constexpr int kApplyItems = 4;          // consecutive records per thread
-constexpr int kApplyPerBlock = kApplyThreads * kApplyItems;
+constexpr int kApplyItemsMax = 4;       // records per thread (striped), chosen per launch: 1, 2 or 4
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
 constexpr uint32_t kTimingStride = 16;          // time every 16th apply launch
@@ -407,6 +406,7 @@ __global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64
 // (A blocked 4-consecutive-records layout with dwordx4 stream loads measured the
 // same on the fan-in and 20 % slower on cfg2, whose new ids are consecutive.)
 // =============================================================================
+template <int kApplyItems>
 __global__ __launch_bounds__(kApplyThreads) void k_apply(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
     const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     // striped: record q of this thread = base + q * 256 + tid, so a wave's q-th
     // access covers 64 consecutive records (coalesced streams; consecutive new ids
     // give coalesced rows)
-    const uint64_t base = beg + (uint64_t)blockIdx.x * kApplyPerBlock + threadIdx.x;
+    const uint64_t base = beg + (uint64_t)blockIdx.x * (kApplyThreads * kApplyItems) + threadIdx.x;
     uint32_t k[kApplyItems], r[kApplyItems], v[kApplyItems];
     int64_t l[kApplyItems];
     bool in[kApplyItems];
@@ -691,6 +691,7 @@ struct crdt_ctx {
     // per-call plan (set by scan, used by later phases)
     uint32_t plan_R = 0;
     uint64_t plan_tiles = 0;
+    int apply_items = 0;            // K2 records per thread; 0 = by changeset size (CRDT_APPLY_ITEMS: tuning)
     // timing
     bool timing = false;
     std::vector<hipEvent_t> events;
@@ -923,8 +924,18 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
         const bool timed = c->timing && (nl++ % kTimingStride) == 0;
         c->apply_total++;
         if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
-        k_apply<<<grid_for(e - b, kApplyPerBlock), kApplyThreads, 0, c->stream>>>(
-            cols.key, cols.lt, cols.rank, cols.val, b, e, j, c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        // records per thread: enough workgroups to cover the 256 CUs several times over
+        const int items = c->apply_items ? c->apply_items : ((e - b) >= (4ull << 20) ? 4 : (e - b) >= (1ull << 20) ? 2 : 1);
+        const unsigned grid = grid_for(e - b, (uint64_t)kApplyThreads * items);
+        if (items == 4)
+            k_apply<4><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        else if (items == 2)
+            k_apply<2><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        else
+            k_apply<1><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
         if (timed) ev_record(c, ev_base + 2 + 2 * (size_t)j);
     }
     HIPCHK(hipGetLastError());
@@ -1008,6 +1019,10 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (!c) return CRDT_E_NOMEM;
     c->device = device;
     c->local_rank = local_rank;
+    if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
+        const int v = atoi(e);
+        c->apply_items = (v == 1 || v == 2 || v == 4) ? v : 0;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_misc, sizeof(Misc)) != hipSuccess ||
         hipHostMalloc(&c->h_misc, sizeof(Misc), hipHostMallocDefault) != hipSuccess ||
