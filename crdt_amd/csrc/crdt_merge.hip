@@ -38,7 +38,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kTile = kScanThreads * kScanItems; // 4096 records per scan tile
 constexpr int kApplyThreads = 256;
-constexpr int kApplyItemsMax = 4;       // records per thread (striped), chosen per launch: 1, 2 or 4
+// K2 records per thread (striped) are chosen per launch: 1, 2, 4 or 8
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
 constexpr uint32_t kTimingStride = 16;          // time every 16th apply launch
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
-    int64_t wall, uint32_t local_rank, long long* __restrict__ M,
+    int64_t wall, uint32_t local_rank,
     int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
 {
     __shared__ int64_t s_max[kScanThreads / 64];
@@ -165,12 +165,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             int tf = s_flag[0];
             for (int k = 1; k < kScanThreads / 64; ++k) { tm = imax(tm, s_max[k]); tf |= s_flag[k]; }
             T[t0 + t] = tm;
-            atomicMax(&M[j], (long long)tm);
             if (tf) {
                 const uint32_t c = atomicAdd(&misc->cand_count, 1u);
                 cand_tile[c] = t0 + t;
             }
         }
+        __syncthreads();
+    }
+}
+
+// M_j = max of changeset j's tile maxima (INT64_MIN when empty).  One block per changeset
+// (grid-stride): no same-address atomics, so a single 10M-record changeset costs what
+// 1024 small ones do.
+__global__ __launch_bounds__(256) void k_tmax(const int64_t* __restrict__ T, const uint32_t* __restrict__ tstart,
+                                              uint32_t R, long long* __restrict__ M)
+{
+    __shared__ int64_t s_max[4];
+    for (uint32_t j = blockIdx.x; j < R; j += gridDim.x) {
+        const uint32_t a = tstart[j], b = tstart[j + 1];
+        int64_t m = INT64_MIN;
+        for (uint32_t t = a + threadIdx.x; t < b; t += 256) m = imax(m, T[t]);
+        m = wave_max(m);
+        if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) M[j] = (long long)imax(imax(s_max[0], s_max[1]), imax(s_max[2], s_max[3]));
         __syncthreads();
     }
 }
@@ -200,7 +218,10 @@ __global__ __launch_bounds__(1024) void k_clock(
     const int64_t W = (int64_t)((uint64_t)wall << kShift);
     int64_t carry = c0;                       // D_0 = C_0
     uint32_t first = UINT32_MAX;
-    if (tid == 0) s_first = UINT32_MAX;
+    if (tid == 0) {
+        s_first = UINT32_MAX;
+        event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN;   // = k_event_init
+    }
     __syncthreads();
     for (uint32_t base = 0; base < R; base += 1024) {
         const uint32_t j = base + tid;
@@ -673,10 +694,10 @@ struct crdt_ctx {
     Misc* h_misc = nullptr;            // pinned
     DBuf<long long> d_M;               // [R]   (single-ctx merge)
     DBuf<long long> d_event;           // [4]
-    DBuf<uint64_t> d_offs;
-    DBuf<uint32_t> d_tstart;
-    HBuf<uint64_t> h_offs;
-    HBuf<uint32_t> h_tstart;
+    DBuf<uint64_t> d_plan;             // offsets[R+1] (u64) then tile starts[R+1] (u32): one H2D copy
+    HBuf<uint64_t> h_plan;
+    const uint64_t* d_offs = nullptr;  // views into d_plan
+    const uint32_t* d_tstart = nullptr;
     DBuf<int64_t> d_T, d_Cprev, d_Rj, d_Cj, d_candP, d_candms;
     DBuf<uint32_t> d_candtile, d_candkind;
     DBuf<long long> d_candkey;
@@ -784,15 +805,16 @@ int stage_apply_cols(crdt_ctx* c, const crdt_batch* b, Cols* cols) {
 // Upload offsets + per-changeset tile starts; returns total tiles and max tiles.
 int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t* max_tiles) {
     const uint32_t R = b->n_changesets;
-    HIPALLOC(c->h_offs.ensure(R + 1));
-    HIPALLOC(c->h_tstart.ensure(R + 1));
-    HIPALLOC(c->d_offs.ensure(R + 1));
-    HIPALLOC(c->d_tstart.ensure(R + 1));
+    const size_t words = (R + 1) + (R + 2) / 2;          // u64 words: offsets, then packed u32 starts
+    HIPALLOC(c->h_plan.ensure(words));
+    HIPALLOC(c->d_plan.ensure(words));
+    uint64_t* h_offs = c->h_plan.p;
+    uint32_t* h_tstart = reinterpret_cast<uint32_t*>(c->h_plan.p + (R + 1));
     uint64_t tiles = 0;
     uint32_t mt = 0;
     for (uint32_t j = 0; j <= R; ++j) {
-        c->h_offs.p[j] = b->offsets[j];
-        c->h_tstart.p[j] = (uint32_t)tiles;
+        h_offs[j] = b->offsets[j];
+        h_tstart[j] = (uint32_t)tiles;
         if (j < R) {
             const uint64_t nj = b->offsets[j + 1] - b->offsets[j];
             const uint64_t tj = (nj + kTile - 1) / kTile;
@@ -801,10 +823,9 @@ int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t*
         }
     }
     if (tiles >= (1ull << 32)) return CRDT_E_INVALID;
-    HIPCHK(hipMemcpyAsync(c->d_offs.p, c->h_offs.p, (R + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_tstart.p, c->h_tstart.p, (R + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_plan.p, c->h_plan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    c->d_offs = c->d_plan.p;
+    c->d_tstart = reinterpret_cast<const uint32_t*>(c->d_plan.p + (R + 1));
     *tiles_out = tiles;
     *max_tiles = mt;
     return CRDT_OK;
@@ -836,8 +857,9 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     HIPALLOC(c->d_candkind.ensure(tiles + 1));
     HIPALLOC(c->d_candms.ensure(tiles + 1));
     if ((st = reset_misc(c))) return st;
-    k_fill_i64<<<grid_for(std::max<uint32_t>(R, 1), 256), 256, 0, c->stream>>>(d_maxima, std::max<uint32_t>(R, 1),
-                                                                                 INT64_MIN);
+    if (!tiles)
+        k_fill_i64<<<grid_for(std::max<uint32_t>(R, 1), 256), 256, 0, c->stream>>>(d_maxima, std::max<uint32_t>(R, 1),
+                                                                                     INT64_MIN);
     c->plan_R = R;
     c->plan_tiles = tiles;
     if (tiles) {
@@ -847,9 +869,10 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
             k_scan<<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
-                cols.lt, cols.rank, cols.millis, c->d_offs.p, c->d_tstart.p, jb, c->canonical, wall,
-                c->local_rank, d_maxima, c->d_T.p, c->d_misc, c->d_candtile.p);
+                cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
         }
+        k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);
         HIPCHK(hipGetLastError());
     }
     return CRDT_OK;
@@ -873,12 +896,12 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
         HIPCHK(hipMemcpyAsync(c->d_ibase.p, c->h_ibase.p, R * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
         d_ibase = c->d_ibase.p;
     }
-    k_event_init<<<1, 64, 0, c->stream>>>(d_event);
+    if (!R) k_event_init<<<1, 64, 0, c->stream>>>(d_event);   // else k_clock initialises the words
     if (R) k_clock<<<1, 1024, 0, c->stream>>>(d_maxima, R, wall, c->canonical, c->d_Cprev.p, c->d_Rj.p,
                                               c->d_Cj.p, d_event);
     if (c->plan_tiles)
         k_verify<<<kVerifyBlocks, 64, 0, c->stream>>>(
-            cols.lt, cols.rank, cols.millis, c->d_offs.p, c->d_tstart.p, R, c->d_T.p, c->d_Cprev.p, wall,
+            cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, R, c->d_T.p, c->d_Cprev.p, wall,
             c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
             c->d_candms.p, d_pbase, d_ibase, d_event);
     HIPCHK(hipGetLastError());
@@ -925,9 +948,13 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
         c->apply_total++;
         if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
         // records per thread: enough workgroups to cover the 256 CUs several times over
-        const int items = c->apply_items ? c->apply_items : ((e - b) >= (4ull << 20) ? 4 : (e - b) >= (1ull << 20) ? 2 : 1);
+        // (measured: more gathers in flight per thread beats more workgroups, down to ~100K records)
+        const int items = c->apply_items ? c->apply_items : ((e - b) >= (512ull << 10) ? 4 : 2);
         const unsigned grid = grid_for(e - b, (uint64_t)kApplyThreads * items);
-        if (items == 4)
+        if (items == 8)
+            k_apply<8><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
+                                                              c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
+        else if (items == 4)
             k_apply<4><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
                                                               c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
         else if (items == 2)
@@ -1021,7 +1048,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     c->local_rank = local_rank;
     if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
         const int v = atoi(e);
-        c->apply_items = (v == 1 || v == 2 || v == 4) ? v : 0;
+        c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_misc, sizeof(Misc)) != hipSuccess ||
@@ -1044,8 +1071,8 @@ void crdt_destroy(crdt_ctx* c) {
     if (c->table) hipFree(c->table);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
-    c->d_M.release(); c->d_event.release(); c->d_offs.release(); c->d_tstart.release();
-    c->h_offs.release(); c->h_tstart.release();
+    c->d_M.release(); c->d_event.release(); c->d_plan.release();
+    c->h_plan.release();
     c->d_T.release(); c->d_Cprev.release(); c->d_Rj.release(); c->d_Cj.release();
     c->d_candP.release(); c->d_candms.release(); c->d_candtile.release(); c->d_candkind.release();
     c->d_candkey.release();

@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for cfg in fanin cfg3 cfg5; do
-  for it in 0 1 2 4; do
+  for it in ${ITEMS:-0 1 2 4}; do
     CRDT_APPLY_ITEMS=$it timeout -k 10 300 python -u bench.py --config $cfg --steps 3 --warmup 1 --no-cpu --no-census \
       > gpurun_out/tune_${cfg}_$it.json 2> gpurun_out/tune_${cfg}_$it.log
     rc=$?; [ $rc -eq 0 ] || { echo "[$cfg items=$it] exit $rc"; tail -5 gpurun_out/tune_${cfg}_$it.log; exit $rc; }
