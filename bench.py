@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--zipf", type=float, default=0.8)
     p.add_argument("--order", choices=["shuffled", "ascending"], default="shuffled")
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    p.add_argument("--route", action="store_true",
+                   help="N > 1: changeset j arrives whole on rank j %% N; records are routed to their owner "
+                        "with RCCL all-to-all inside the timed step (north star config 4)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
@@ -77,16 +80,28 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    from crdt_amd.dist import sharded_merge, sharded_merge_parts, torch_all_gather, torch_reducers
+    from crdt_amd.dist import (sharded_merge, sharded_merge_parts, sharded_merge_routed, torch_all_gather,
+                               torch_all_to_all, torch_alloc, torch_reducers)
     if world > 1:
         red_max, red_min = torch_reducers(dist)
         gather = torch_all_gather(dist)
+        a2a = torch_all_to_all(dist)
+        alloc = torch_alloc(dev)
     from crdt_amd import DeviceTable
     from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
 
     t0 = time.time()
     weak = world > 1 and args.scaling == "weak"
-    if args.config == "fanin" and weak:
+    route = world > 1 and args.route
+    if args.config == "fanin" and route:
+        m = world if weak else 1
+        wl = gen_fanin(total=args.records * m, R=args.replicas, K=args.keys * m, n_local=args.local * m,
+                       s=args.zipf, device=dev, order=args.order, rank=rank, world=world, route=True)
+        workload = (f"fanin routed x{world} ({'weak' if weak else 'strong'}): {wl['total']:,} records = "
+                    f"{wl['R']} replicas x {wl['n_per_replica']:,}, replica j on rank j % {world}, Zipf({args.zipf}) "
+                    f"keys over {m}·2^{int(np.log2(args.keys))} ids routed to owner key % {world} by RCCL "
+                    f"all-to-all, local map {m}·2^{int(np.log2(args.local))} keys")
+    elif args.config == "fanin" and weak:
         # this rank's part: a full single-GPU fan-in over its own 2^28 slots (global key = slot*N + rank)
         wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
                        device=dev, order=args.order, rank=0, world=1, seed=0xC0FFEE04 + 7919 * rank)
@@ -128,8 +143,11 @@ def main():
     loc = wl["local"]
     own, home = wl["owned"], wl["home"]
     own_cols = (own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], None)
-    home_cols = (own["key"][:0] if world > 1 else own["key"], home["lt"], home["rank"],
-                 own["val"][:0] if world > 1 else own["val"], wl["home_offsets"], None)
+    if route:
+        home_cols = (home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], None)
+    else:
+        home_cols = (own["key"][:0] if world > 1 else own["key"], home["lt"], home["rank"],
+                     own["val"][:0] if world > 1 else own["val"], wl["home_offsets"], None)
     R = wl["R"]
     d_max = torch.zeros(max(R, 1), dtype=torch.int64, device=dev)
     d_ev = torch.zeros(4, dtype=torch.int64, device=dev)
@@ -162,6 +180,9 @@ def main():
         if world == 1:
             res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
             return res
+        if route:
+            return sharded_merge_routed(table, home_cols, wl["wall"], d_max, d_ev, red_max, red_min, gather,
+                                        a2a, rank, world, alloc, win_flags=flags)
         if weak:
             # per changeset: part scan -> all-gather maxima -> clock -> MIN(event) -> resolve -> MAX -> apply
             return sharded_merge_parts(table, own_cols, wl["wall"], wl["index_base"], d_max, d_ev, gather,
@@ -211,7 +232,7 @@ def main():
     value = total_records / (ms_per_step / 1e3)
 
     # ---- per-kernel roofline of K2 (apply): algorithmic bytes / event-timed duration
-    n_owned = int(wl["owned_offsets"][-1])
+    n_owned = int(res.get("n_recv", wl["owned_offsets"][-1]))            # routed: records received
     kb = 20 * n_owned + 12 * res["n_present"] + 24 * res["n_won"]          # per step, this rank
     launches_per_step = max(apply_total // max(args.steps, 1), 1)
     alg_per_launch = kb / launches_per_step
@@ -262,7 +283,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "weak" if (world == 1 or weak) else "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
         "config": {"workload": workload, "records": total_records, "replicas": R,
-                   "parallelism": (f"keyshard{world}-{'parts' if weak else 'home'}" if world > 1 else "single"),
+                   "parallelism": (f"keyshard{world}-{'routed' if route else 'parts' if weak else 'home'}"
+                                   if world > 1 else "single"),
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),

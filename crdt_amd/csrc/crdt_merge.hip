@@ -487,6 +487,84 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     }
 }
 
+// =============================================================================
+// Routing (multi-GPU, records arrive on their changeset's home rank): partition a
+// batch by owner rank key % G into per-(owner, changeset) chunks of the send
+// columns, slot = key / G.  Order inside a chunk is not preserved (keys are
+// unique within a changeset, so K2 is order-independent inside one); the
+// optional perm column gives each sent record's index in the batch.
+// =============================================================================
+constexpr int kRouteMaxRanks = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void k_route_count(
+    const uint32_t* __restrict__ key, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
+    uint32_t jbase, uint32_t G, unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t s_cnt[kRouteMaxRanks];
+    const uint32_t j = jbase + blockIdx.y;
+    const uint64_t beg = offs[j], end = offs[j + 1];
+    const uint32_t nt = tstart[j + 1] - tstart[j];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
+        __syncthreads();
+        const uint64_t base = beg + (uint64_t)t * kTile;
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            if (i < end) atomicAdd(&s_cnt[key[i] % G], 1u);
+        }
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
+            if (s_cnt[d]) atomicAdd(&counts[(uint64_t)j * G + d], (unsigned long long)s_cnt[d]);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_route_scatter(
+    const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
+    uint32_t jbase, uint32_t G, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ o_slot,
+    int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank, uint32_t* __restrict__ o_val,
+    uint64_t* __restrict__ o_perm)
+{
+    __shared__ uint32_t s_cnt[kRouteMaxRanks];
+    __shared__ unsigned long long s_base[kRouteMaxRanks];
+    const uint32_t j = jbase + blockIdx.y;
+    const uint64_t beg = offs[j], end = offs[j + 1];
+    const uint32_t nt = tstart[j + 1] - tstart[j];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
+        __syncthreads();
+        const uint64_t base = beg + (uint64_t)t * kTile;
+        uint32_t dst[kScanItems], pos[kScanItems];
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            if (i < end) {
+                dst[q] = key[i] % G;
+                pos[q] = atomicAdd(&s_cnt[dst[q]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
+            s_base[d] = s_cnt[d] ? atomicAdd(&cursor[(uint64_t)j * G + d], (unsigned long long)s_cnt[d]) : 0;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            if (i < end) {
+                const uint64_t o = s_base[dst[q]] + pos[q];
+                o_slot[o] = key[i] / G;
+                o_lt[o] = lt[i];
+                o_rank[o] = rank[i];
+                o_val[o] = val[i];
+                if (o_perm) o_perm[o] = i;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ----------------------------------------------------------------- SPI kernels
 __global__ __launch_bounds__(256) void k_put_rows(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
@@ -694,6 +772,9 @@ struct crdt_ctx {
     Misc* h_misc = nullptr;            // pinned
     DBuf<long long> d_M;               // [R]   (single-ctx merge)
     DBuf<long long> d_event;           // [4]
+    DBuf<uint64_t> d_rplan;            // routing: offsets + tile starts of the routed batch
+    HBuf<uint64_t> h_rplan;
+    DBuf<unsigned long long> d_rcount; // routing: [R][G] counts, then cursors
     DBuf<uint64_t> d_plan;             // offsets[R+1] (u64) then tile starts[R+1] (u32): one H2D copy
     HBuf<uint64_t> h_plan;
     const uint64_t* d_offs = nullptr;  // views into d_plan
@@ -915,18 +996,14 @@ int phase_resolve(crdt_ctx* c, long long* d_event) {
     return CRDT_OK;
 }
 
-int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long long* d_event,
-                uint8_t* win_flags, crdt_result* out, size_t ev_base) {
-    int st = validate_batch(owned);
-    if (st) return st;
+// K2 over changeset ranges: changeset j's records are [beg[j], fin[j]) of the columns (host arrays).
+// n = length of the columns (win flags are indexed like them).
+int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint64_t* fin, uint64_t n, int32_t mem,
+                 int64_t wall, const long long* d_event, uint8_t* win_flags, crdt_result* out, size_t ev_base) {
     const uint32_t R = c->plan_R;
-    if (owned->n_changesets != R) return CRDT_E_INVALID;
-    Cols cols;
-    if ((st = stage_apply_cols(c, owned, &cols))) return st;
-    const uint64_t n = owned->offsets[R];
     uint8_t* dflags = nullptr;
     if (win_flags) {
-        if (owned->mem == CRDT_MEM_DEVICE) {
+        if (mem == CRDT_MEM_DEVICE) {
             dflags = win_flags;
         } else {
             HIPALLOC(c->s_flags.ensure(n ? n : 1));
@@ -940,15 +1017,15 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     uint32_t nl = 0;
     c->apply_total = 0;
     for (uint32_t j = 0; j < R; ++j) {
-        const uint64_t b = owned->offsets[j], e = owned->offsets[j + 1];
+        const uint64_t b = beg[j], e = fin[j];
         if (e == b) continue;
         // HIP-event timing of a sample of the launches (every kTimingStride-th): per-launch
         // durations without perturbing the rest of the stream
         const bool timed = c->timing && (nl++ % kTimingStride) == 0;
         c->apply_total++;
         if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
-        // records per thread: enough workgroups to cover the 256 CUs several times over
-        // (measured: more gathers in flight per thread beats more workgroups, down to ~100K records)
+        // records per thread (measured: more gathers in flight per thread beats more
+        // workgroups, down to ~100K records per changeset)
         const int items = c->apply_items ? c->apply_items : ((e - b) >= (512ull << 10) ? 4 : 2);
         const unsigned grid = grid_for(e - b, (uint64_t)kApplyThreads * items);
         if (items == 8)
@@ -967,7 +1044,7 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-    if (win_flags && owned->mem == CRDT_MEM_HOST && n)
+    if (win_flags && mem == CRDT_MEM_HOST && n)
         HIPCHK(hipMemcpyAsync(win_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     crdt_result res = c->h_misc->result;
@@ -979,6 +1056,43 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     c->canonical = res.canonical_lt;
     if (out) *out = res;
     return res.status;
+}
+
+int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long long* d_event,
+                uint8_t* win_flags, crdt_result* out, size_t ev_base) {
+    int st = validate_batch(owned);
+    if (st) return st;
+    const uint32_t R = c->plan_R;
+    if (owned->n_changesets != R) return CRDT_E_INVALID;
+    Cols cols;
+    if ((st = stage_apply_cols(c, owned, &cols))) return st;
+    return apply_ranges(c, cols, owned->offsets, owned->offsets + 1, owned->offsets[R], owned->mem, wall, d_event,
+                        win_flags, out, ev_base);
+}
+
+// Upload a batch's offsets + tile starts into the routing plan (kept apart from the merge plan).
+int upload_route_plan(crdt_ctx* c, const crdt_batch* b, uint32_t* max_tiles) {
+    const uint32_t R = b->n_changesets;
+    const size_t words = (R + 1) + (R + 2) / 2;
+    HIPALLOC(c->h_rplan.ensure(words));
+    HIPALLOC(c->d_rplan.ensure(words));
+    uint64_t* h_offs = c->h_rplan.p;
+    uint32_t* h_tstart = reinterpret_cast<uint32_t*>(c->h_rplan.p + (R + 1));
+    uint64_t tiles = 0;
+    uint32_t mt = 0;
+    for (uint32_t j = 0; j <= R; ++j) {
+        h_offs[j] = b->offsets[j];
+        h_tstart[j] = (uint32_t)tiles;
+        if (j < R) {
+            const uint64_t tj = (b->offsets[j + 1] - b->offsets[j] + kTile - 1) / kTile;
+            tiles += tj;
+            mt = std::max<uint32_t>(mt, (uint32_t)tj);
+        }
+    }
+    if (tiles >= (1ull << 32)) return CRDT_E_INVALID;
+    HIPCHK(hipMemcpyAsync(c->d_rplan.p, c->h_rplan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    *max_tiles = mt;
+    return CRDT_OK;
 }
 
 void collect_timing(crdt_ctx* c, uint32_t R, bool full) {
@@ -1389,6 +1503,90 @@ int crdt_merge_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const u
     }
     collect_timing(c, R, true);
     return st;
+}
+
+int crdt_merge_apply_segments(crdt_ctx* c, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
+                              const uint32_t* val, uint64_t n, const uint64_t* seg_begin, const uint64_t* seg_end,
+                              int64_t wall, const uint64_t* d_event, uint8_t* win_flags, crdt_result* out) {
+    if (!c || !d_event) return CRDT_E_INVALID;
+    const uint32_t R = c->plan_R;
+    if (R && (!seg_begin || !seg_end)) return CRDT_E_INVALID;
+    for (uint32_t j = 0; j < R; ++j)
+        if (seg_begin[j] > seg_end[j] || seg_end[j] > n) return CRDT_E_INVALID;
+    if (n && (!key_id || !lt || !rank || !val)) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    Cols cols;
+    cols.key = key_id; cols.lt = lt; cols.rank = rank; cols.val = val;
+    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
+    ev_record(c, 2);
+    int st = apply_ranges(c, cols, seg_begin, seg_end, n, CRDT_MEM_DEVICE, wall,
+                          reinterpret_cast<const long long*>(d_event), win_flags, out, 3);
+    if (c->timing) {
+        ev_record(c, 3 + 2 * (size_t)R + 1);
+        hipStreamSynchronize(c->stream);
+    }
+    collect_timing(c, R, true);
+    return st;
+}
+
+int crdt_route_count(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, uint64_t* counts) {
+    if (!c || !counts || n_ranks == 0 || n_ranks > (uint32_t)kRouteMaxRanks) return CRDT_E_INVALID;
+    int st = validate_batch(batch);
+    if (st) return st;
+    const uint32_t R = batch->n_changesets;
+    const uint64_t n = batch->offsets[R];
+    if (n && !batch->key_id) return CRDT_E_INVALID;
+    const size_t cells = (size_t)R * n_ranks;
+    if (!cells) return CRDT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t* key;
+    if ((st = stage(c, c->s_key, batch->key_id, n, batch->mem, &key))) return st;
+    uint32_t mt = 0;
+    if ((st = upload_route_plan(c, batch, &mt))) return st;
+    HIPALLOC(c->d_rcount.ensure(cells));
+    HIPCHK(hipMemsetAsync(c->d_rcount.p, 0, cells * sizeof(unsigned long long), c->stream));
+    const uint64_t* offs = c->d_rplan.p;
+    const uint32_t* tstart = reinterpret_cast<const uint32_t*>(c->d_rplan.p + (R + 1));
+    if (mt) {
+        const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, std::max<uint32_t>(1, 65536u / R)));
+        for (uint32_t jb = 0; jb < R; jb += 65535)
+            k_route_count<<<dim3(gx, std::min<uint32_t>(65535, R - jb)), kScanThreads, 0, c->stream>>>(
+                key, offs, tstart, jb, n_ranks, c->d_rcount.p);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(counts, c->d_rcount.p, cells * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_route_scatter(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, const uint64_t* send_base,
+                       uint32_t* out_slot, int64_t* out_lt, uint32_t* out_rank, uint32_t* out_val,
+                       uint64_t* out_perm) {
+    if (!c || n_ranks == 0 || n_ranks > (uint32_t)kRouteMaxRanks) return CRDT_E_INVALID;
+    int st = validate_batch(batch);
+    if (st) return st;
+    const uint32_t R = batch->n_changesets;
+    const uint64_t n = batch->offsets[R];
+    if (!n) return CRDT_OK;
+    if (!send_base || !out_slot || !out_lt || !out_rank || !out_val) return CRDT_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    Cols cols;
+    if ((st = stage_apply_cols(c, batch, &cols))) return st;
+    uint32_t mt = 0;
+    if ((st = upload_route_plan(c, batch, &mt))) return st;
+    const size_t cells = (size_t)R * n_ranks;
+    HIPALLOC(c->d_rcount.ensure(cells));
+    HIPCHK(hipMemcpyAsync(c->d_rcount.p, send_base, cells * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    const uint64_t* offs = c->d_rplan.p;
+    const uint32_t* tstart = reinterpret_cast<const uint32_t*>(c->d_rplan.p + (R + 1));
+    const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, std::max<uint32_t>(1, 65536u / R)));
+    for (uint32_t jb = 0; jb < R; jb += 65535)
+        k_route_scatter<<<dim3(gx, std::min<uint32_t>(65535, R - jb)), kScanThreads, 0, c->stream>>>(
+            cols.key, cols.lt, cols.rank, cols.val, offs, tstart, jb, n_ranks, c->d_rcount.p, out_slot, out_lt,
+            out_rank, out_val, out_perm);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
 }
 
 int crdt_set_timing(crdt_ctx* c, int enable) {

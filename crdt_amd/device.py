@@ -239,6 +239,38 @@ class DeviceTable:
                     "crdt_merge_apply")
         return res.as_dict()
 
+    # ---------------------------------------------- routed multi-GPU (all-to-all)
+    def route_count(self, batch, n_ranks: int) -> np.ndarray:
+        """[R, n_ranks] uint64: records of changeset j owned by rank d (key % n_ranks)."""
+        b, c, offs = self._batch(*batch)
+        R = len(offs) - 1
+        out = np.zeros((R, n_ranks), np.uint64)
+        self._check(self._lib.crdt_route_count(self._ctx, ctypes.byref(b), n_ranks,
+                                               out.ctypes.data_as(ctypes.c_void_p)), "crdt_route_count")
+        return out
+
+    def route_scatter(self, batch, n_ranks: int, send_base, out_slot, out_lt, out_rank, out_val, out_perm=None):
+        """Partition ``batch`` into the device send columns; chunk (j, d) starts at send_base[j, d]."""
+        b, c, _ = self._batch(*batch)
+        base = np.ascontiguousarray(send_base, dtype=np.uint64)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self._lib.crdt_route_scatter(
+            self._ctx, ctypes.byref(b), n_ranks, base.ctypes.data_as(ctypes.c_void_p), P(out_slot), P(out_lt),
+            P(out_rank), P(out_val), None if out_perm is None else P(out_perm)), "crdt_route_scatter")
+
+    def merge_apply_segments(self, cols, seg_begin, seg_end, wall: int, d_event, win_flags=None) -> dict:
+        """Apply phase over device columns (key_slot, lt, rank, val); changeset j = [seg_begin[j], seg_end[j])."""
+        key, lt, rank, val = cols
+        sb = np.ascontiguousarray(seg_begin, dtype=np.uint64)
+        se = np.ascontiguousarray(seg_end, dtype=np.uint64)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        res = CrdtResult()
+        self._check(self._lib.crdt_merge_apply_segments(
+            self._ctx, P(key), P(lt), P(rank), P(val), int(key.numel()), sb.ctypes.data_as(ctypes.c_void_p),
+            se.ctypes.data_as(ctypes.c_void_p), int(wall), P(d_event),
+            None if win_flags is None else P(win_flags), ctypes.byref(res)), "crdt_merge_apply_segments")
+        return res.as_dict()
+
     # ---------------------------------------------------------------- timing
     def set_timing(self, enable: bool):
         self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")

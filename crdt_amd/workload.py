@@ -54,7 +54,9 @@ def _zipf_keys(n: int, rows: int, K: int, s: float, gen: torch.Generator, device
 def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_local: int = 1 << 27,
               s: float = 0.8, seed: int = 0xC0FFEE04, device="cuda", order: str = "shuffled",
               rank: int = 0, world: int = 1, chunk: int = 64, millis_span: int = 1 << 16,
-              counter_span: int = 16) -> dict:
+              counter_span: int = 16, route: bool = False) -> dict:
+    """``route``: records are NOT pre-split by owner — this rank keeps the full changesets it is
+    home to (``home`` gets key and val too, ``owned`` is empty) for the routed protocol."""
     dev = torch.device(device)
     n = -(-total // R)                                   # records per replica (ceil)
     wall = BASE_MILLIS + millis_span + 1000
@@ -83,7 +85,12 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
             if world > 1 and j % world == rank:
                 home["lt"].append(lt[r_].clone())
                 home["rank"].append(rk[r_].to(torch.int32))
+                if route:
+                    home.setdefault("key", []).append(key[r_].to(torch.int32))
+                    home.setdefault("val", []).append(val.expand(rows, n)[r_].to(torch.int32))
                 home_counts[j] = n
+            if route:
+                continue
             if world == 1:
                 m = slice(None)
                 k_own = key[r_]
@@ -96,8 +103,10 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
             own["val"].append(val.expand(rows, n)[r_][m].to(torch.int32))
             own_counts[j] = own["key"][-1].numel()
         del key, lt, rk, val
-    cat = lambda xs: torch.cat(xs) if xs else torch.zeros(0, device=dev)  # noqa: E731
+    cat = lambda xs: torch.cat(xs) if xs else torch.zeros(0, device=dev, dtype=torch.int32)  # noqa: E731
     owned = {k: cat(v) for k, v in own.items()}
+    if route:
+        owned["lt"] = owned["lt"].to(torch.int64)
     del own
     if world == 1:                                       # one rank is home to every changeset
         homed = {"lt": owned["lt"], "rank": owned["rank"]}

@@ -178,6 +178,29 @@ int crdt_merge_resolve(crdt_ctx* ctx, const crdt_batch* home, uint64_t* d_event)
 int crdt_merge_apply(crdt_ctx* ctx, const crdt_batch* owned, int64_t wall_millis,
                      const uint64_t* d_event, uint8_t* win_flags, crdt_result* out);
 
+/* ---- routed multi-GPU (records arrive on their changeset's home rank) -------
+ * North star config 4 / SURVEY §8(e) step 5: the home rank partitions its batch by
+ * owner rank d = key_id % n_ranks (slot key_id / n_ranks), the host exchanges the
+ * chunks with RCCL all-to-all, and each owner applies changeset j from wherever its
+ * records landed.  No reference counterpart (the reference is single-process).
+ *
+ * crdt_route_count: counts[j * n_ranks + d] = records of changeset j owned by d (HOST out).
+ * crdt_route_scatter: writes the batch's records into the send columns (DEVICE), chunk
+ *   (j, d) starting at send_base[j * n_ranks + d] (HOST in); order inside a chunk is
+ *   unspecified; out_perm (optional) receives each sent record's index in the batch.
+ * crdt_merge_apply_segments: the apply phase over DEVICE columns of length n where
+ *   changeset j is rows [seg_begin[j], seg_end[j]) (HOST arrays of the plan's R);
+ *   win_flags (optional, DEVICE [n]) indexed like the columns.  Same result as
+ *   crdt_merge_apply. */
+int crdt_route_count(crdt_ctx* ctx, const crdt_batch* batch, uint32_t n_ranks, uint64_t* counts);
+int crdt_route_scatter(crdt_ctx* ctx, const crdt_batch* batch, uint32_t n_ranks, const uint64_t* send_base,
+                       uint32_t* out_slot, int64_t* out_lt, uint32_t* out_rank, uint32_t* out_val,
+                       uint64_t* out_perm);
+int crdt_merge_apply_segments(crdt_ctx* ctx, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
+                              const uint32_t* val, uint64_t n, const uint64_t* seg_begin,
+                              const uint64_t* seg_end, int64_t wall_millis, const uint64_t* d_event,
+                              uint8_t* win_flags, crdt_result* out);
+
 /* ---- measurement ---------------------------------------------------------- */
 int crdt_set_timing(crdt_ctx* ctx, int enable);
 int crdt_get_timing(const crdt_ctx* ctx, crdt_timing* out);

@@ -18,6 +18,11 @@ I64MAX = np.iinfo(np.int64).max
 LOW = (1 << 40) - 1
 
 
+def _np(t):
+    """numpy view of a numpy array or a CPU torch tensor (shared memory)."""
+    return t.numpy() if hasattr(t, "numpy") else t
+
+
 def _send_fails(r, wall):
     m, c = r >> SHIFT, r & MAXC
     mn = max(m, wall)
@@ -93,11 +98,44 @@ class PhaseModel:
         if ev in self.cands:
             d_ev[1], d_ev[2], d_ev[3] = self.cands[ev]
 
+    # routing (k_route_count / k_route_scatter): owner d = key % G, slot = key // G
+    def route_count(self, batch, G):
+        key, _, _, _, offs, _ = batch
+        offs = np.asarray(offs, np.int64)
+        out = np.zeros((len(offs) - 1, G), np.uint64)
+        for j in range(len(offs) - 1):
+            out[j] = np.bincount(np.asarray(key[offs[j]:offs[j + 1]], np.int64) % G, minlength=G)
+        return out
+
+    def route_scatter(self, batch, G, send_base, o_slot, o_lt, o_rank, o_val, out_perm=None):
+        key, lt, rank, val, offs, _ = batch
+        offs = np.asarray(offs, np.int64)
+        o = [_np(o_slot).view(np.uint32), _np(o_lt), _np(o_rank).view(np.uint32), _np(o_val).view(np.uint32)]
+        perm = None if out_perm is None else _np(out_perm)
+        cur = np.asarray(send_base, np.int64).copy()
+        for j in range(len(offs) - 1):
+            for x in range(offs[j], offs[j + 1]):            # (the device order inside a chunk differs)
+                d = int(key[x]) % G
+                at = cur[j, d]
+                cur[j, d] += 1
+                o[0][at], o[1][at], o[2][at], o[3][at] = int(key[x]) // G, lt[x], rank[x], val[x]
+                if perm is not None:
+                    perm[at] = x
+
+    def merge_apply_segments(self, cols, seg_begin, seg_end, wall, d_ev, win_flags=None):
+        key, lt, rank, val = (_np(c) for c in cols)
+        fl = None if win_flags is None else _np(win_flags)
+        return self._apply(key.view(np.uint32), lt, rank.view(np.uint32), val.view(np.uint32),
+                           np.asarray(seg_begin, np.int64), np.asarray(seg_end, np.int64), wall, d_ev, fl)
+
     # K3d + K2
     def merge_apply(self, owned, wall, d_ev, win_flags=None):
         key, lt, rank, val, offs, _ = owned
         offs = np.asarray(offs, np.int64)
-        R = len(offs) - 1
+        return self._apply(key, lt, rank, val, offs[:-1], offs[1:], wall, d_ev, win_flags)
+
+    def _apply(self, key, lt, rank, val, begin, end, wall, d_ev, win_flags):
+        R = len(begin)
         ev = int(d_ev[0])
         res = dict(status=0, n_stored=R, exc_changeset=0, exc_index=(1 << 64) - 1, drift_ms=0, counter=0,
                    n_present=0, n_won=0)
@@ -117,7 +155,7 @@ class PhaseModel:
                     res["drift_ms"] = int(d_ev[3]) - wall
         res["n_stored"] = stop
         for j in range(stop):
-            for x in range(offs[j], offs[j + 1]):
+            for x in range(begin[j], end[j]):
                 k = int(key[x])
                 present = self.mod[k] >= 0
                 win = (not present) or lt[x] > self.lt[k] or (lt[x] == self.lt[k] and rank[x] > self.rank[k])

@@ -208,3 +208,88 @@ def test_parts_protocol_equals_single_table(name):
             assert np.array_equal(a[slots], orows[f][mine]), f
     assert tot == [ores["n_present"], ores["n_won"]]
     assert np.array_equal(flags, oflags)
+
+
+# ---------------------------------------------------------------- routed protocol (all-to-all)
+def _home_batch(case, world, rank):
+    """Changesets j % world == rank in full (keys included), the others empty."""
+    offs = case["offsets"]
+    R = len(offs) - 1
+    sel = np.concatenate([np.arange(offs[j], offs[j + 1]) for j in range(R) if j % world == rank] or
+                         [np.zeros(0, np.int64)]).astype(np.int64)
+    hc = np.where(np.arange(R) % world == rank, np.diff(offs.astype(np.int64)), 0)
+    home_offs = np.concatenate([[0], np.cumsum(hc)]).astype(np.uint64)
+    millis = case["millis"]
+    return (case["key"][sel], case["lt"][sel], case["rank"][sel], case["val"][sel], home_offs,
+            None if millis is None else millis[sel]), sel
+
+
+def _routed_worker(rank, world, port, case_kw, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from crdt_amd.dist import sharded_merge_routed, torch_all_gather, torch_all_to_all, torch_alloc
+        case = make_case(**case_kw)
+        cap = -(-case["n_ids"] // world)
+        t = PhaseModel(cap, case["local_rank"], case["c0"])
+        loc = case["local"]
+        ids = np.arange(case["n_local"])
+        mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
+        t.put_rows(ids[mine] // world, loc["lt"][mine], loc["rank"][mine], loc["val"][mine], loc["mod"][mine])
+        home, sel = _home_batch(case, world, rank)
+        R = len(case["offsets"]) - 1
+        d_max = torch.zeros(max(R, 1), dtype=torch.int64)
+        d_ev = torch.zeros(4, dtype=torch.int64)
+        flags = torch.zeros(len(sel), dtype=torch.uint8)
+        red_max, red_min = torch_reducers(dist)
+        res = sharded_merge_routed(t, home, case["wall"], d_max, d_ev, red_max, red_min, torch_all_gather(dist),
+                                   torch_all_to_all(dist), rank, world, torch_alloc("cpu"), win_flags=flags)
+        q.put((rank, res, t.lt, t.rank, t.val, t.mod, sel, flags.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,world", [("r4_ties", 2), ("dup_node", 2), ("drift_late", 2), ("send_overflow", 2),
+                                        ("r8_tombstones", 3), ("explicit_millis", 2), ("empty_changesets", 2)])
+def test_routed_protocol_equals_single_table(name, world):
+    kw = dict(CASE_SPECS)[name]
+    case = make_case(**kw)
+    orows, ores, oflags = oracle_run(case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_routed_worker, args=(r, world, port, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    flags = np.zeros(len(case["key"]), np.uint8)
+    tot = [0, 0]
+    for rank, res, lt, rk, val, mod, sel, fl in outs:
+        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
+            assert res[f] == ores[f], (name, rank, f, res[f], ores[f])
+        tot[0] += res["n_present"]
+        tot[1] += res["n_won"]
+        flags[sel] = fl
+        keys = np.arange(case["n_ids"])
+        mine = keys % world == rank
+        slots = keys[mine] // world
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a[slots], orows[f][mine]), f
+    assert tot == [ores["n_present"], ores["n_won"]]
+    assert np.array_equal(flags, oflags)
+
+
+def test_route_plan_layout():
+    from crdt_amd.dist import route_plan
+    # 2 ranks, 3 changesets: rank 0 holds j = 0, 2; rank 1 holds j = 1
+    ca = np.zeros((2, 3, 2), np.int64)
+    ca[0, 0] = [3, 2]
+    ca[0, 2] = [1, 4]
+    ca[1, 1] = [5, 0]
+    sb, ss, rs, b, e = route_plan(ca, 0)
+    assert ss.tolist() == [4, 6] and rs.tolist() == [4, 5]
+    assert sb[:, 0].tolist() == [0, 3, 3] and sb[:, 1].tolist() == [4, 6, 6]
+    assert b.tolist() == [0, 4, 3] and e.tolist() == [3, 9, 4]

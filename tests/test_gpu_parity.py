@@ -234,3 +234,121 @@ def test_two_rank_sharded_on_device(gpu_device, name, protocol):
             assert np.array_equal(a[slots], orows[f][mine]), f
     assert tot == [ores["n_present"], ores["n_won"]]
     assert np.array_equal(flags, oflags)
+
+
+def _routed_gpu_worker(rank, world, port, case_kw, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.dist import sharded_merge_routed, torch_all_gather, torch_all_to_all, torch_alloc, torch_reducers
+    from tests.test_dist_cpu import _home_batch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = make_case(**case_kw)
+        cap = -(-case["n_ids"] // world)
+        t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
+        loc = case["local"]
+        ids = np.arange(case["n_local"])
+        mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
+        if mine.any():
+            t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
+                       loc["val"][mine], loc["mod"][mine])
+        t.canonical = case["c0"]
+        home, sel = _home_batch(case, world, rank)
+        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        home_d = (dev(home[0]), dev(home[1]), dev(home[2]), dev(home[3]), home[4], dev(home[5]))
+        R = len(case["offsets"]) - 1
+        d_max = torch.zeros(max(R, 1), dtype=torch.int64, device="cuda")
+        d_ev = torch.zeros(4, dtype=torch.int64, device="cuda")
+        flags = torch.zeros(len(sel), dtype=torch.uint8, device="cuda")
+        red_max, red_min = torch_reducers(dist)
+        res = sharded_merge_routed(t, home_d, case["wall"], d_max, d_ev, red_max, red_min, torch_all_gather(dist),
+                                   torch_all_to_all(dist), rank, world, torch_alloc("cuda"), win_flags=flags)
+        lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
+        q.put((rank, res, lt, rk, val, mod, sel, flags.cpu().numpy()))
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
+def test_two_rank_routed_on_device(gpu_device, name):
+    """Routed protocol on device: k_route_count / k_route_scatter, all-to-all, segmented K2."""
+    import torch.multiprocessing as mp
+
+    from tests.test_dist_cpu import _free_port
+    kw = dict(CASE_SPECS)[name]
+    case = make_case(**kw)
+    orows, ores, oflags = oracle_run(case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_routed_gpu_worker, args=(r, 2, port, kw, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    flags = np.zeros(len(case["key"]), np.uint8)
+    tot = [0, 0]
+    for rank, res, lt, rk, val, mod, sel, fl in outs:
+        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
+            assert res[f] == ores[f], (name, rank, f)
+        tot[0] += res["n_present"]
+        tot[1] += res["n_won"]
+        flags[sel] = fl
+        keys = np.arange(case["n_ids"])
+        mine = keys % 2 == rank
+        slots = keys[mine] // 2
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a[slots], orows[f][mine]), f
+    assert tot == [ores["n_present"], ores["n_won"]]
+    assert np.array_equal(flags, oflags)
+
+
+def test_route_kernels_partition(gpu_device):
+    """k_route_count / k_route_scatter on a 3M-record, 5-changeset batch for 8 owners: counts,
+    chunk contents (as multisets) and perm against numpy."""
+    import torch
+
+    from crdt_amd import DeviceTable
+    rng = np.random.default_rng(3)
+    R, G = 5, 8
+    sizes = [700_001, 0, 1_200_000, 4097, 1_095_902]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    n = int(offs[-1])
+    key = rng.integers(0, 1 << 30, n, dtype=np.uint32)
+    lt = rng.integers(0, 1 << 60, n, dtype=np.int64)
+    rank = rng.integers(0, 1000, n, dtype=np.uint32)
+    val = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    t = DeviceTable(0, capacity=16)
+    d = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).cuda()  # noqa: E731
+    batch = (d(key), d(lt), d(rank), d(val), offs, None)
+    counts = t.route_count(batch, G)
+    exp = np.zeros((R, G), np.uint64)
+    for j in range(R):
+        exp[j] = np.bincount(key[offs[j]:offs[j + 1]] % G, minlength=G)
+    assert np.array_equal(counts, exp)
+    ca = counts.astype(np.int64)[None]                       # a single holder: rank 0 of a 1-rank view
+    sb = (np.concatenate([[0], np.cumsum(ca[0].sum(axis=0))[:-1]])[None, :] + np.cumsum(ca[0], axis=0) - ca[0])
+    outs = [torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int64, device="cuda"),
+            torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda")]
+    perm = torch.empty(n, dtype=torch.int64, device="cuda")
+    t.route_scatter(batch, G, sb.astype(np.uint64), *outs, out_perm=perm)
+    slot, olt, ork, ov = (o.cpu().numpy() for o in outs)
+    p = perm.cpu().numpy()
+    assert np.array_equal(np.sort(p), np.arange(n))          # a permutation
+    assert np.array_equal(slot.view(np.uint32), key[p] // G)
+    assert np.array_equal(olt, lt[p]) and np.array_equal(ork.view(np.uint32), rank[p])
+    assert np.array_equal(ov.view(np.uint32), val[p])
+    for j in range(R):                                       # chunk (j, d) holds exactly its records
+        for g in range(G):
+            a, c = int(sb[j, g]), int(counts[j, g])
+            seg = p[a:a + c]
+            assert np.all((seg >= offs[j]) & (seg < offs[j + 1])) and np.all(key[seg] % G == g)
+    t.close()
