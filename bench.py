@@ -273,9 +273,10 @@ def main():
         del flags
 
     # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
-    cpu = None
+    cpu = cpu_omp = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wl, args.cpu_seconds)
+        cpu_omp = cpu_baseline_omp(wl, args.cpu_seconds)
 
     out = {
         "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
@@ -286,7 +287,7 @@ def main():
                    "parallelism": (f"keyshard{world}-{'routed' if route else 'parts' if weak else 'home'}"
                                    if world > 1 else "single"),
                    "step_ms_all": [round(x, 3) for x in step_ms]},
-        "roofline": roofline, "job": job, "cpu_baseline": cpu,
+        "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
                          "apply_kernels_est": round(avg_launch_us * launches_per_step / 1e3, 3),
                          "apply_launches": launches_per_step,
@@ -333,6 +334,42 @@ def cpu_baseline(wl, budget_s):
             "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged into the full "
                       f"{cap:,}-row map by oracle/merge_oracle.c in faithful mode (one full map copy per "
                       f"merge, map_crdt.dart:43; one clock read per record, hlc.dart:82), {el:.1f}s"}
+
+
+def cpu_baseline_omp(wl, budget_s):
+    """Times oracle/merge_omp.c (the optimised multi-core merge, same results) on the leading
+    changesets of the same workload, 16 changesets per call, within ~budget_s seconds."""
+    import torch
+    from oracle.oracle_c import OracleTable
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    loc = wl["local"]
+    t = OracleTable(wl["capacity"], 0, wl["c0"])
+    t.put_rows(loc["slot"].cpu().numpy().astype(np.uint32), loc["lt"].cpu().numpy(),
+               loc["rank"].cpu().numpy().astype(np.uint32), loc["val"].cpu().numpy().astype(np.uint32),
+               loc["mod"].cpu().numpy())
+    offs, own = wl["owned_offsets"], wl["owned"]
+    per_call = wl.get("per_call", False)
+    step = 1 if per_call else 16
+    done, recs, el = 0, 0, 0.0
+    while done < wl["R"] and el < budget_s:
+        j1 = min(done + step, wl["R"])
+        b, e = int(offs[done]), int(offs[j1])
+        cols = [own[k][b:e].cpu().numpy() for k in ("key", "lt", "rank", "val")]
+        sub = (offs[done:j1 + 1] - offs[done]).astype(np.uint64)
+        wall = int(wl["walls"][done]) if per_call else wl["wall"]
+        ts = time.perf_counter()
+        res, _ = t.merge_omp(cols[0].astype(np.uint32), cols[1], cols[2].astype(np.uint32),
+                             cols[3].astype(np.uint32), sub, wall, threads=threads, want_flags=False)
+        el += time.perf_counter() - ts
+        assert res.status == 0
+        done = j1
+        recs += e - b
+    del t
+    torch.cuda.synchronize()
+    return {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
+                      f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
+                      f"{threads} OpenMP threads, {el:.1f}s"}
 
 
 if __name__ == "__main__":

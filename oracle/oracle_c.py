@@ -50,6 +50,8 @@ def lib():
         L.or_merge.argtypes = [P, ctypes.c_uint64, P, ctypes.c_uint32, P, P, P, P, P, P,
                                ctypes.c_uint32, ctypes.c_int64, P, ctypes.c_int, P]
         L.or_merge.restype = ctypes.c_int
+        L.or_merge_omp.argtypes = L.or_merge.argtypes
+        L.or_merge_omp.restype = ctypes.c_int
         L.or_put_stamped.argtypes = [P, ctypes.c_uint64, P, ctypes.c_uint32, P, P, ctypes.c_uint64,
                                      ctypes.c_int64, P]
         L.or_put_stamped.restype = ctypes.c_int
@@ -97,6 +99,23 @@ class OracleTable:
         self.rows["val"][key] = val
         self.rows["mod"][key] = mod
         self.rows["aux"][key] = 0
+
+    def merge_omp(self, key, lt, rank, val, offsets, wall, millis=None, threads=0, want_flags=True):
+        """oracle/merge_omp.c: the optimised multi-core baseline (same results as merge())."""
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        lt = np.ascontiguousarray(lt, dtype=np.int64)
+        rank = np.ascontiguousarray(rank, dtype=np.uint32)
+        val = np.ascontiguousarray(val, dtype=np.uint32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        millis = None if millis is None else np.ascontiguousarray(millis, dtype=np.int64)
+        flags = np.zeros(int(offsets[-1]), dtype=np.uint8) if want_flags else None
+        res = OrResult()
+        st = lib().or_merge_omp(_p(self.rows), len(self.rows), _p(self._canon), self.local_rank,
+                                _p(key), _p(lt), _p(rank), _p(val), _p(millis), _p(offsets),
+                                len(offsets) - 1, wall, _p(flags), int(threads), ctypes.byref(res))
+        if st < 0:
+            raise ValueError(f"oracle error {st}")
+        return res, flags
 
     def merge(self, key, lt, rank, val, offsets, wall, millis=None, faithful=False, want_flags=True):
         key = np.ascontiguousarray(key, dtype=np.uint32)

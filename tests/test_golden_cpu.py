@@ -69,3 +69,23 @@ def test_faithful_mode_same_results():
 
 def test_absent_pattern():
     assert ABSENT_MOD < 0
+
+
+@pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
+def test_omp_baseline_equals_sequential(name):
+    """oracle/merge_omp.c (the multi-core CPU baseline) == or_merge on every case."""
+    from oracle.oracle_c import OracleTable
+    from tests._cases import ABSENT_MOD, oracle_run
+    case = make_case(**dict(CASE_SPECS)[name])
+    orows, ores, oflags = oracle_run(case)
+    t = OracleTable(case["n_ids"], case["local_rank"], case["c0"])
+    loc = case["local"]
+    keep = loc["mod"] != ABSENT_MOD
+    ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
+    t.put_rows(ids, loc["lt"][keep], loc["rank"][keep], loc["val"][keep], loc["mod"][keep])
+    res, flags = t.merge_omp(case["key"], case["lt"], case["rank"], case["val"], case["offsets"], case["wall"],
+                             millis=case["millis"], threads=4)
+    assert res.as_dict() == ores
+    assert np.array_equal(flags, oflags)
+    for f in ("lt", "rank", "val", "mod"):
+        assert np.array_equal(t.rows[f], orows[f]), f
