@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--route", action="store_true",
                    help="N > 1: changeset j arrives whole on rank j %% N; records are routed to their owner "
                         "with RCCL all-to-all inside the timed step (north star config 4)")
+    p.add_argument("--path", choices=["auto", "gather", "sorted"], default="auto",
+                   help="merge strategy (crdt_set_merge_path): gather = K2 per changeset, sorted = key-partitioned")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
@@ -140,6 +142,7 @@ def main():
     log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
 
     table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
+    table.set_merge_path(args.path)
     loc = wl["local"]
     own, home = wl["owned"], wl["home"]
     own_cols = (own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], None)

@@ -487,6 +487,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     }
 }
 
+#include "sorted_path.inc"
+
 // =============================================================================
 // Routing (multi-GPU, records arrive on their changeset's home rank): partition a
 // batch by owner rank key % G into per-(owner, changeset) chunks of the send
@@ -799,6 +801,16 @@ struct crdt_ctx {
     std::vector<hipEvent_t> events;
     std::vector<uint32_t> launched;
     uint32_t apply_total = 0;
+    // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
+    int merge_path = 0;
+    DBuf<u32x4> p1_rec, p2_rec;        // 16-B partitioned records {lt, rank, val}
+    DBuf<uint32_t> p1_kj, p2_kj;       // and their kj words
+    DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
+    DBuf<uint64_t> p_plan, p_l1beg;
+    DBuf<uint32_t> p_ibase, p_ksu32, p_tseg, p_ibucket;   // resolve items per bucket; part-state / carry u32 columns
+    DBuf<int64_t> p_kslt;
+    HBuf<uint64_t> h_pplan;
+    bool last_sorted = false;       // the last crdt_merge ran the sorted path
     crdt_timing last_timing{};
 };
 
@@ -1058,14 +1070,156 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
     return res.status;
 }
 
+// Sorted path (sorted_path.inc) for the whole batch: k_resolve (stop point), then per
+// window of kWindow changesets a level-1 (+ level-2) stable partition of the applied
+// records and the per-bucket LDS resolve.  offs = host offsets of the batch, whose
+// device copy c->d_offs was uploaded by phase_scan for this same batch.
+int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wall, const long long* d_event,
+                 crdt_result* out, size_t ev_base) {
+    const uint32_t R = c->plan_R;
+    k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    ev_record(c, ev_base);
+    c->launched.clear();
+    c->apply_total = 1;
+    if (c->timing) { c->launched.push_back(0); ev_record(c, ev_base + 1); }
+    const bool two = c->cap > (1ull << 20);
+    const uint32_t shift1 = two ? 20u : (uint32_t)kSBits;
+    for (uint32_t jb = 0; jb < R; jb += kWindow) {
+        const uint32_t je = std::min<uint32_t>(R, jb + kWindow);
+        const uint32_t nseg = je - jb;
+        const uint64_t nw = offs[je] - offs[jb];
+        if (nw == 0) continue;
+        // host plan: level-1 tile prefix over the window's changesets + the one-segment scan map
+        // (the pinned staging buffer is reused: the previous window's copy must have run)
+        if (jb > 0) HIPCHK(hipStreamSynchronize(c->stream));
+        const size_t tb_words = (nseg + 2) / 2;
+        HIPALLOC(c->h_pplan.ensure(tb_words + 3));
+        HIPALLOC(c->p_plan.ensure(tb_words + 3));
+        uint32_t* tb = reinterpret_cast<uint32_t*>(c->h_pplan.p);
+        uint32_t nt1 = 0;
+        for (uint32_t s = 0; s <= nseg; ++s) {
+            tb[s] = nt1;
+            if (s < nseg) nt1 += (uint32_t)((offs[jb + s + 1] - offs[jb + s] + kPTile - 1) / kPTile);
+        }
+        const uint32_t nc1 = (nt1 + kChunkTiles - 1) / kChunkTiles;
+        uint32_t* sm_t = reinterpret_cast<uint32_t*>(c->h_pplan.p + tb_words);
+        sm_t[0] = 0; sm_t[1] = nt1;                                   // scan tbase {0, nt1}
+        uint32_t* sm_c = reinterpret_cast<uint32_t*>(c->h_pplan.p + tb_words + 1);
+        sm_c[0] = 0; sm_c[1] = nc1;                                   // scan cbase {0, nc1}
+        c->h_pplan.p[tb_words + 2] = 0;                               // seg_pos {0}
+        HIPCHK(hipMemcpyAsync(c->p_plan.p, c->h_pplan.p, (tb_words + 3) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              c->stream));
+        const uint32_t nt2 = two ? (uint32_t)((nw + kPTile - 1) / kPTile) + kDigits : 0;
+        const uint32_t nc2 = two ? (nt2 + kChunkTiles - 1) / kChunkTiles + kDigits : 0;
+        const uint32_t ntm = std::max(nt1, nt2), ncm = std::max(nc1, nc2);
+        HIPALLOC(c->p_hist.ensure((size_t)ntm * kDigits));
+        HIPALLOC(c->p_toff.ensure((size_t)ntm * kDigits));
+        HIPALLOC(c->p_part.ensure((size_t)ncm * kDigits));
+        HIPALLOC(c->p_choff.ensure((size_t)ncm * kDigits));
+        HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
+        HIPALLOC(c->p1_rec.ensure(nw)); HIPALLOC(c->p1_kj.ensure(nw));
+        const uint32_t* d_tb1 = reinterpret_cast<const uint32_t*>(c->p_plan.p);
+        HIPALLOC(c->p_tseg.ensure(ntm));
+        k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1, c->p_tseg.p);
+        const TileMap tm1{c->d_offs + jb, d_tb1, c->p_tseg.p, nseg};
+        const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words),
+                          reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words + 1), c->p_plan.p + tb_words + 2, 1};
+        if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
+        k_part_hist<true><<<nt1, kPThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1, c->p_hist.p);
+        k_scan_part<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, sm1, c->p_part.p);
+        k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
+                                             two ? c->p_l1beg.p : nullptr);
+        k_scan_tiles<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
+        k_part_scatter<true><<<nt1, kPThreads, 0, c->stream>>>(
+            cols.key, cols.lt, cols.rank, cols.val, nullptr, nullptr, tm1, jb, c->d_misc, c->cap, shift1,
+            c->p_toff.p, c->p1_rec.p, c->p1_kj.p);
+        if (two) {
+            HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
+            HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
+            HIPALLOC(c->p2_rec.ensure(nw)); HIPALLOC(c->p2_kj.ensure(nw));
+            uint32_t* tb2 = c->p_l2map.p;
+            uint32_t* cb2 = c->p_l2map.p + kDigits + 1;
+            k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2);
+            k_seg_index<<<std::min<uint32_t>(grid_for(nt2, 256), 4096), 256, 0, c->stream>>>(tb2, kDigits, nt2,
+                                                                                            c->p_tseg.p);
+            const TileMap tm2{c->p_l1beg.p, tb2, c->p_tseg.p, kDigits};
+            const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
+            k_part_hist<false><<<nt2, kPThreads, 0, c->stream>>>(
+                c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
+                                                                  c->p_hist.p);
+            k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
+            k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
+            k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
+            k_part_scatter<false><<<nt2, kPThreads, 0, c->stream>>>(
+                nullptr, nullptr, nullptr, nullptr, c->p1_rec.p, c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
+                c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
+        }
+        // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
+        const uint32_t nb = two ? kDigits * kDigits : kDigits;
+        const uint32_t* bst = two ? c->p_dstart2.p : c->p_dstart1.p;
+        const u32x4* rec = two ? c->p2_rec.p : c->p1_rec.p;
+        const uint32_t* rv = two ? c->p2_kj.p : c->p1_kj.p;
+        const uint32_t max_items = nb + (uint32_t)(nw / kRPart) + 1;
+        const size_t ksn = (size_t)(2 * (nw / kRPart) + 2) * kSKeys;     // part-state slots of split buckets
+        HIPALLOC(c->p_ibase.ensure(2 * (nb + 1)));
+        HIPALLOC(c->p_kslt.ensure(2 * ksn));
+        HIPALLOC(c->p_ksu32.ensure(6 * ksn));
+        uint32_t* d_ib = c->p_ibase.p;
+        uint32_t* d_hb = c->p_ibase.p + nb + 1;
+        KeyState ps{c->p_kslt.p, c->p_ksu32.p, c->p_ksu32.p + ksn, c->p_ksu32.p + 2 * ksn};
+        KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
+        HIPALLOC(c->p_ibucket.ensure(max_items));
+        k_bucket_items<<<1, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb);
+        k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
+                                                                                               c->p_ibucket.p);
+        k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv, c->table,
+                                                                c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
+        k_part_carry<<<dim3(kSKeys / 256, nb), 256, 0, c->stream>>>(bst, d_ib, d_hb, nb, c->table, c->cap, ps, cy);
+        k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
+                                                                 c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
+        HIPCHK(hipGetLastError());
+    }
+    if (c->timing) ev_record(c, ev_base + 2);
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    crdt_result res = c->h_misc->result;
+    uint64_t np = 0, nw_ = 0;
+    for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw_ += c->h_misc->won[s]; }
+    res.n_present = np;
+    res.n_won = nw_;
+    if (c->h_misc->err) res.status = CRDT_E_KEY_RANGE;
+    c->canonical = res.canonical_lt;
+    if (out) *out = res;
+    return res.status;
+}
+
+// The sorted path runs for crdt_merge when its preconditions hold (sorted_path.inc
+// header) and either CRDT_MERGE_PATH=sorted or the batch is a multi-changeset fan-in
+// large enough to amortise the partition passes.
+bool use_sorted(const crdt_ctx* c, const crdt_batch* b, const uint8_t* win_flags) {
+    if (c->merge_path == 1 || win_flags || c->canonical < 0 || c->cap > kSortedMaxCap) return false;
+    const uint32_t R = b->n_changesets;
+    for (uint32_t jb = 0; jb < R; jb += kWindow) {
+        const uint32_t je = std::min<uint32_t>(R, jb + kWindow);
+        if (b->offsets[je] - b->offsets[jb] >= (1ull << 31)) return false;
+    }
+    if (c->merge_path == 2) return true;
+    // auto: many small changesets (cfg3-like fan-in), where one partitioned pass beats R
+    // latency-bound K2 launches; large changesets keep K2 (measured)
+    const uint64_t n = b->offsets[R];
+    return R >= 64 && n >= (8ull << 20) && n / R <= (256ull << 10);
+}
+
 int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long long* d_event,
-                uint8_t* win_flags, crdt_result* out, size_t ev_base) {
+                uint8_t* win_flags, crdt_result* out, size_t ev_base, bool allow_sorted = false) {
     int st = validate_batch(owned);
     if (st) return st;
     const uint32_t R = c->plan_R;
     if (owned->n_changesets != R) return CRDT_E_INVALID;
     Cols cols;
     if ((st = stage_apply_cols(c, owned, &cols))) return st;
+    c->last_sorted = allow_sorted && use_sorted(c, owned, win_flags);
+    if (c->last_sorted) return apply_sorted(c, cols, owned->offsets, wall, d_event, out, ev_base);
     return apply_ranges(c, cols, owned->offsets, owned->offsets + 1, owned->offsets[R], owned->mem, wall, d_event,
                         win_flags, out, ev_base);
 }
@@ -1160,6 +1314,9 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (!c) return CRDT_E_NOMEM;
     c->device = device;
     c->local_rank = local_rank;
+    if (const char* e = getenv("CRDT_MERGE_PATH")) {
+        c->merge_path = strcmp(e, "gather") == 0 ? 1 : strcmp(e, "sorted") == 0 ? 2 : 0;
+    }
     if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
         const int v = atoi(e);
         c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
@@ -1195,6 +1352,12 @@ void crdt_destroy(crdt_ctx* c) {
     c->d_word.release();
     c->d_ibase.release();
     c->h_ibase.release();
+    c->p1_rec.release(); c->p1_kj.release(); c->p2_rec.release(); c->p2_kj.release();
+    c->p_hist.release(); c->p_toff.release(); c->p_part.release(); c->p_choff.release();
+    c->p_dstart1.release(); c->p_dstart2.release(); c->p_l2map.release();
+    c->p_plan.release(); c->p_l1beg.release(); c->h_pplan.release();
+    c->p_ibase.release(); c->p_ksu32.release(); c->p_kslt.release(); c->p_tseg.release();
+    c->p_ibucket.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -1443,7 +1606,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
     if ((st = phase_resolve(c, c->d_event.p))) return st;
     ev_record(c, 2);
-    st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, 3);
+    st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, 3, true);
     if (c->timing) {
         ev_record(c, 3 + 2 * (size_t)R + 1);
         hipStreamSynchronize(c->stream);
@@ -1586,6 +1749,18 @@ int crdt_route_scatter(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, c
             out_rank, out_val, out_perm);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_set_merge_path(crdt_ctx* c, int path) {
+    if (!c || path < CRDT_PATH_AUTO || path > CRDT_PATH_SORTED) return CRDT_E_INVALID;
+    c->merge_path = path;
+    return CRDT_OK;
+}
+
+int crdt_last_path(const crdt_ctx* c, int* path) {
+    if (!c || !path) return CRDT_E_INVALID;
+    *path = c->last_sorted ? CRDT_PATH_SORTED : CRDT_PATH_GATHER;
     return CRDT_OK;
 }
 

@@ -272,6 +272,17 @@ class DeviceTable:
         return res.as_dict()
 
     # ---------------------------------------------------------------- timing
+    PATHS = {"auto": 0, "gather": 1, "sorted": 2}
+
+    def set_merge_path(self, path: str):
+        """'auto' | 'gather' | 'sorted' (crdt_set_merge_path): the strategy of later merges."""
+        self._check(self._lib.crdt_set_merge_path(self._ctx, self.PATHS[path]), "crdt_set_merge_path")
+
+    def last_path(self) -> str:
+        v = ctypes.c_int(0)
+        self._check(self._lib.crdt_last_path(self._ctx, ctypes.byref(v)), "crdt_last_path")
+        return {1: "gather", 2: "sorted"}[v.value]
+
     def set_timing(self, enable: bool):
         self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")
 

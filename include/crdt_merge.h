@@ -201,6 +201,20 @@ int crdt_merge_apply_segments(crdt_ctx* ctx, const uint32_t* key_id, const int64
                               const uint64_t* seg_end, int64_t wall_millis, const uint64_t* d_event,
                               uint8_t* win_flags, crdt_result* out);
 
+/* ---- merge strategy --------------------------------------------------------
+ * crdt_merge resolves a batch either by the gather path (one launch per changeset,
+ * every record reads its row: K2) or by the sorted path (the applied records are
+ * partitioned by key into 4096-key buckets, each bucket's rows are read and written
+ * once and its records resolved in LDS; sorted_path.inc).  Both give identical
+ * rows, canonical, status and counts.  The sorted path needs: win_flags == NULL,
+ * canonical >= 0, capacity <= 2^28.  path: CRDT_PATH_AUTO (default, also set by the
+ * CRDT_MERGE_PATH environment variable = gather | sorted), CRDT_PATH_GATHER,
+ * CRDT_PATH_SORTED (whenever allowed).  crdt_last_path reports the path the last
+ * crdt_merge took (CRDT_PATH_GATHER or CRDT_PATH_SORTED). */
+enum crdt_path { CRDT_PATH_AUTO = 0, CRDT_PATH_GATHER = 1, CRDT_PATH_SORTED = 2 };
+int crdt_set_merge_path(crdt_ctx* ctx, int path);
+int crdt_last_path(const crdt_ctx* ctx, int* path);
+
 /* ---- measurement ---------------------------------------------------------- */
 int crdt_set_timing(crdt_ctx* ctx, int enable);
 int crdt_get_timing(const crdt_ctx* ctx, crdt_timing* out);

@@ -12,9 +12,13 @@ RESULT_FIELDS = ("status", "n_stored", "exc_changeset", "exc_index", "canonical_
                  "n_present", "n_won")
 
 
-def device_run(case, device_cols=False, capacity=None):
+def device_run(case, device_cols=False, capacity=None, path=None, flags=True):
+    """path: None (auto) | 'gather' | 'sorted' (crdt_set_merge_path); flags=False asks for no
+    per-record win flags (the sorted path's precondition), returned flags are then None."""
     from crdt_amd import DeviceTable
     t = DeviceTable(0, local_rank=case["local_rank"], capacity=capacity or case["n_ids"])
+    if path:
+        t.set_merge_path(path)
     loc = case["local"]
     keep = loc["mod"] != ABSENT_MOD
     ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
@@ -27,13 +31,14 @@ def device_run(case, device_cols=False, capacity=None):
         import torch
         cols = [torch.from_numpy(c.astype(c.dtype)).cuda() for c in cols]
         millis = None if millis is None else torch.from_numpy(millis).cuda()
-    res, flags = t.merge(*cols, case["offsets"], case["wall"], millis=millis)
-    if device_cols:
-        flags = flags.cpu().numpy()
+    res, fl = t.merge(*cols, case["offsets"], case["wall"], millis=millis, win_flags=flags)
+    if device_cols and fl is not None:
+        fl = fl.cpu().numpy()
     lt, rank, val, mod = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
     assert t.canonical == res["canonical_lt"]
+    res["path"] = t.last_path()
     t.close()
-    return (lt, rank, val, mod), res, flags
+    return (lt, rank, val, mod), res, fl
 
 
 @pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
@@ -51,7 +56,8 @@ def compare_with_oracle(case, **kw):
     orows, ores, oflags = oracle_run(case)
     for f, a in zip(("lt", "rank", "val", "mod"), rows):
         assert np.array_equal(a, orows[f]), f
-    assert np.array_equal(flags, oflags)
+    if flags is not None:
+        assert np.array_equal(flags, oflags)
     for k in RESULT_FIELDS:
         assert res[k] == ores[k], (k, res[k], ores[k])
     return res
@@ -352,3 +358,122 @@ def test_route_kernels_partition(gpu_device):
             seg = p[a:a + c]
             assert np.all((seg >= offs[j]) & (seg < offs[j + 1])) and np.all(key[seg] % G == g)
     t.close()
+
+
+# ------------------------------------------------------------------ sorted path
+# The key-partitioned path (sorted_path.inc) against the same oracle: rows, canonical,
+# status, exception fields and the per-record counts n_present / n_won.
+def _sorted_expected(case):
+    """The sorted path runs iff its preconditions hold (no flags, C0 >= 0)."""
+    return "sorted" if case["c0"] >= 0 else "gather"
+
+
+@pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
+def test_sorted_golden_vectors(gpu_device, name):
+    case, exp, expected = golden_case(name)
+    rows, res, flags = device_run(case, path="sorted", flags=False)
+    check_rows(*rows, exp)
+    assert flags is None
+    for k, v in expected.items():
+        assert res[k] == v, (name, k, res[k], v)
+    assert res["path"] == _sorted_expected(case)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_sorted_random_small(gpu_device, seed):
+    rng = np.random.default_rng(1000 + seed)
+    kw = dict(seed=2000 + seed, R=int(rng.integers(1, 12)), per_cs=int(rng.integers(0, 500)),
+              n_local=int(rng.integers(1, 600)), n_new=int(rng.integers(0, 400)),
+              millis_span=int(rng.integers(1, 100)), counter_span=int(rng.integers(1, 8)),
+              n_ranks=int(rng.integers(2, 40)), tomb_frac=float(rng.random() * 0.5),
+              neg_mod_frac=float(rng.random() * 0.1), dup_frac=float(rng.random() * 0.01),
+              drift_frac=float(rng.random() * 0.005))
+    kw["local_rank"] = int(rng.integers(0, kw["n_ranks"]))
+    case = make_case(**kw)
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["path"] == _sorted_expected(case)
+
+
+@pytest.mark.parametrize("capacity", [None, (1 << 20) + 7, 1 << 24])
+def test_sorted_ties_many_changesets(gpu_device, capacity):
+    """300 tie-heavy changesets (same key in many of them, equal (lt, rank) across them):
+    one-level buckets (capacity <= 2^20) and two-level (capacity > 2^20)."""
+    case = make_case(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8,
+                     counter_span=4, n_ranks=301)
+    res = compare_with_oracle(case, path="sorted", flags=False, capacity=capacity)
+    assert res["path"] == "sorted" and res["n_won"] > 0
+
+
+def test_sorted_hot_keys_in_one_chunk(gpu_device):
+    """Few keys, many changesets: every 2048-record chunk holds dozens of records per key,
+    so the in-chunk same-key lists are long (ordering inside a chunk)."""
+    case = make_case(seed=83, R=400, per_cs=60, n_local=50, n_new=30, millis_span=3, counter_span=2,
+                     n_ranks=7)
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["path"] == "sorted"
+
+
+def test_sorted_split_hot_bucket(gpu_device):
+    """All keys in one 4096-key bucket, 240K records: the bucket is resolved as 4 parts
+    (part folds, carries, per-part counts) — ties and tombstones across the part cuts."""
+    case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                     n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["path"] == "sorted" and res["n_won"] > 0
+
+
+def test_sorted_windows_and_late_exception(gpu_device):
+    """More changesets than one 4096-changeset window; a drift record in changeset 4500
+    stops the batch there (later windows and changesets untouched)."""
+    case = make_case(seed=84, R=5000, per_cs=20, n_local=3000, n_new=2000, millis_span=20,
+                     force=[(4500, 7, "drift")])
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["status"] == 1 and res["exc_changeset"] == 4500 and res["path"] == "sorted"
+
+
+def test_sorted_large_single_changeset(gpu_device):
+    from tests._cases import WALL
+    case = make_case(seed=78, R=1, per_cs=1_000_000, n_local=1_200_000, n_new=800_000,
+                     millis_span=1 << 16, base=WALL - 70_000)
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["status"] == 0 and res["path"] == "sorted"
+
+
+def test_sorted_key_out_of_range(gpu_device):
+    from crdt_amd import CrdtNativeError, DeviceTable
+    t = DeviceTable(0, local_rank=0, capacity=64)
+    t.set_merge_path("sorted")
+    with pytest.raises(CrdtNativeError):
+        t.merge(np.array([1, 10_000], np.uint32), np.array([5, 6], np.int64), np.array([1, 1], np.uint32),
+                np.array([0, 0], np.uint32), np.array([0, 2], np.uint64), 1 << 40, win_flags=False)
+    assert t.last_path() == "sorted"
+
+
+@pytest.mark.parametrize("K,total,R", [(1 << 20, 3_000_000, 64), (1 << 24, 8_000_000, 96)])
+def test_sorted_equals_gather_fanin(gpu_device, K, total, R):
+    """Full-table property check at a fan-in shape (Zipf keys, unique per replica, hot head):
+    both paths from the same state give the same rows, canonical and counts."""
+    import torch
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    own, loc = wl["owned"], wl["local"]
+    out = {}
+    for path in ("gather", "sorted"):
+        t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+        t.set_merge_path(path)
+        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        t.canonical = wl["c0"]
+        res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                         win_flags=False)
+        assert t.last_path() == path
+        rows = t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))
+        out[path] = (res, rows)
+        t.close()
+    (rg, ag), (rs, as_) = out["gather"], out["sorted"]
+    for k in RESULT_FIELDS:
+        assert rg[k] == rs[k], (k, rg[k], rs[k])
+    for a, b in zip(ag, as_):
+        assert np.array_equal(a, b)
+    torch.cuda.empty_cache()
