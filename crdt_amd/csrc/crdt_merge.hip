@@ -1125,7 +1125,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words),
                           reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words + 1), c->p_plan.p + tb_words + 2, 1};
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
-        k_part_hist<true><<<nt1, kPThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1, c->p_hist.p);
+        k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1, c->p_hist.p);
         k_scan_part<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, sm1, c->p_part.p);
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
@@ -1144,7 +1144,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
                                                                                             c->p_tseg.p);
             const TileMap tm2{c->p_l1beg.p, tb2, c->p_tseg.p, kDigits};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            k_part_hist<false><<<nt2, kPThreads, 0, c->stream>>>(
+            k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(
                 c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
                                                                   c->p_hist.p);
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
