@@ -83,9 +83,23 @@ class Crdt:
 
     def mergeJson(self, js: str, keyDecoder=None, valueDecoder=None, wall: int | None = None):
         wall = self._wall(wall)                                         # crdt.dart:100-109
+        if keyDecoder is None and valueDecoder is None and self._native_ingest():
+            from . import hostlib
+            n0 = len(self._keys)
+            try:
+                dec = hostlib.decode(js, self._keys.native)             # libcrdt_host.so
+            except (hostlib.Fallback, ValueError):
+                dec = None                                              # the restatement decides
+            if dec is not None:
+                self.last_ingest = "native"
+                return self._merge_decoded(dec, n0, wall)
+        self.last_ingest = "python"
         m = CrdtJson.decode(js, self.canonicalTime, keyDecoder=keyDecoder, valueDecoder=valueDecoder,
                             millis=wall)
         self.merge(m, wall=wall)
+
+    def _native_ingest(self) -> bool:
+        return False
 
     def toJson(self, modifiedSince: Hlc | None = None, keyEncoder=None, valueEncoder=None) -> str:
         return CrdtJson.encode(self.recordMap(modifiedSince=modifiedSince),           # crdt.dart:127-135
@@ -265,6 +279,36 @@ class MapCrdt(Crdt):
         self._maybe_compact()
 
     # ------------------------------------------------------------ merge
+    def _native_ingest(self) -> bool:
+        return self._keys.native is not None and self._nodes.kind in (None, "str")
+
+    def _merge_decoded(self, dec: dict, n0: int, wall: int):
+        """merge() of one natively decoded CrdtJson document (crdt.dart:77-94 on columns):
+        keys already interned (ids >= n0 are new), values still raw JSON text."""
+        kid, lt, nodes = dec["key_id"], dec["lt"], dec["nodes"]
+        n = len(kid)
+        self._register_nodes(nodes)
+        lut = np.array([self._nodes.rank(x) for x in nodes], np.uint32)
+        rank = lut[dec["node"]] if n else np.zeros(0, np.uint32)
+        val = self._values.put_raw(dec["buf"], dec["val_off"], dec["val_len"])
+        self._reserve()
+        res, flags = self._table.merge(kid, lt, rank, val, np.array([0, n], np.uint64), wall)
+        won = flags[:n].astype(bool) if res["n_stored"] else np.zeros(n, bool)
+        if not res["n_stored"]:
+            self._keys.truncate(n0)                    # keys of an unstored changeset never entered
+        self._values.release_many(val[~won & (val != NULL_HANDLE)])
+        if won.any() and (self._hlc_override or self._mod_override):
+            for k in kid[won].tolist():                 # canonical-form Hlc, modified by this node
+                self._hlc_override.pop(k, None)
+                self._mod_override.pop(k, None)
+        if won.any() and self._watches:
+            keys = self._keys.keys
+            for x in np.flatnonzero(won).tolist():
+                self._emit(keys[int(kid[x])], self._values.get(int(val[x])))
+        self._maybe_compact()
+        self._raise_for(res)
+        return res
+
     def merge(self, remoteRecords: dict, wall: int | None = None):    # crdt.dart:77-94
         self.mergeAll([remoteRecords], wall=wall)
 

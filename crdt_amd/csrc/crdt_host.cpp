@@ -1,0 +1,697 @@
+// crdt_host.cpp — native host ingest for the MapCrdt merge path (include/crdt_host.h).
+//
+// The device kernels (crdt_merge.hip) consume integer columns; this file turns the
+// reference's wire format into them without a per-record trip through Python:
+//   * crdt_keys      — key interning (LinkedHashMap order ids, map_crdt.dart:10)
+//   * crdt_json_decode — CrdtJson.decode (crdt_json.dart:19-37) + Record.fromJson
+//                      (record.dart:21-26) + Hlc.parse (hlc.dart:39-46) for the format
+//                      CrdtJson.encode / Hlc.toString write (crdt_json.dart:8-17,
+//                      hlc.dart:101-104); everything else is CRDT_HOST_FALLBACK.
+//   * crdt_hlc_format  — Hlc.toString for a batch of clocks.
+// Built with g++ -O3 (no GPU code).  Parity: tests/test_host_ingest.py compares every
+// column with the Python restatement (crdt_amd/crdt_json.py, crdt_amd/hlc.py).
+#include "crdt_host.h"
+
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr int kShift = 16;                        // hlc.dart:3
+constexpr int64_t kMaxMs = 8640000000000000ll;    // DateTime range (ms)
+
+inline uint64_t hash_bytes(const char* p, uint64_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
+    uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    uint64_t t = 0;
+    for (uint64_t k = 0; i + k < n; ++k) t |= (uint64_t)(uint8_t)p[i + k] << (8 * k);
+    h = (h ^ t) * 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 32;
+    return h ? h : 1;
+}
+
+// Days since 1970-01-01 of a proleptic Gregorian date (any int month/day offsets).
+inline int64_t days_from_civil(int64_t y, int64_t m, int64_t d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * ((m + 9) % 12) + 2) / 5 + d - 1;
+    return era * 146097 + yoe * 365 + yoe / 4 - yoe / 100 + doy - 719468;
+}
+
+inline void civil_from_days(int64_t z, int64_t* y, int64_t* m, int64_t* d) {
+    z += 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    *m = mp < 10 ? mp + 3 : mp - 9;
+    *d = doy - (153 * mp + 2) / 5 + 1;
+    *y = yoe + era * 400 + (*m <= 2);
+}
+
+inline int64_t floordiv(int64_t a, int64_t b) { return a / b - ((a % b != 0) && ((a < 0) != (b < 0))); }
+
+inline int digit(char c) { return (c >= '0' && c <= '9') ? c - '0' : -1; }
+inline int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ key table
+struct crdt_keys {
+    std::vector<char> arena;
+    std::vector<uint64_t> off{0};      // off[id] .. off[id + 1]
+    std::vector<uint64_t> hash;        // per id
+    std::vector<uint32_t> slot;        // open addressing: id + 1, 0 = empty
+    uint64_t mask = 0;
+
+    uint64_t size() const { return hash.size(); }
+
+    void rebuild(uint64_t want) {
+        uint64_t cap = 16;
+        while (cap < want * 2) cap <<= 1;
+        slot.assign(cap, 0);
+        mask = cap - 1;
+        for (uint64_t id = 0; id < hash.size(); ++id) {
+            uint64_t s = hash[id] & mask;
+            while (slot[s]) s = (s + 1) & mask;
+            slot[s] = (uint32_t)(id + 1);
+        }
+    }
+
+    bool find(const char* p, uint64_t n, uint64_t h, uint32_t* id) const {
+        if (slot.empty()) return false;
+        for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+            const uint32_t v = slot[s];
+            if (!v) return false;
+            const uint32_t i = v - 1;
+            if (hash[i] == h && off[i + 1] - off[i] == n && memcmp(arena.data() + off[i], p, n) == 0) {
+                *id = i;
+                return true;
+            }
+        }
+    }
+
+    uint32_t add(const char* p, uint64_t n, uint64_t h) {
+        if ((hash.size() + 1) * 2 > slot.size()) rebuild(hash.size() + 1 > 8 ? (hash.size() + 1) * 2 : 16);
+        const uint32_t id = (uint32_t)hash.size();
+        arena.insert(arena.end(), p, p + n);
+        off.push_back(arena.size());
+        hash.push_back(h);
+        uint64_t s = h & mask;
+        while (slot[s]) s = (s + 1) & mask;
+        slot[s] = id + 1;
+        return id;
+    }
+};
+
+// --------------------------------------------------------------- decode state
+struct crdt_decoded {
+    std::vector<uint32_t> key;
+    std::vector<int64_t> lt;
+    std::vector<uint32_t> node;
+    std::vector<uint64_t> voff;
+    std::vector<uint32_t> vlen;
+    std::vector<std::string> nodes;
+};
+
+namespace {
+
+struct Fallback {};
+struct JsonError {};
+
+struct Parser {
+    const char* s;
+    uint64_t n, i = 0;
+    std::string tmp;
+
+    void ws() {
+        while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) ++i;
+    }
+    char peek() { return i < n ? s[i] : '\0'; }
+    void expect(char c) {
+        if (i >= n || s[i] != c) throw JsonError();
+        ++i;
+    }
+
+    static void put_utf8(std::string& o, uint32_t cp) {
+        if (cp < 0x80) {
+            o += (char)cp;
+        } else if (cp < 0x800) {
+            o += (char)(0xC0 | (cp >> 6));
+            o += (char)(0x80 | (cp & 0x3F));
+        } else if (cp < 0x10000) {
+            o += (char)(0xE0 | (cp >> 12));
+            o += (char)(0x80 | ((cp >> 6) & 0x3F));
+            o += (char)(0x80 | (cp & 0x3F));
+        } else {
+            o += (char)(0xF0 | (cp >> 18));
+            o += (char)(0x80 | ((cp >> 12) & 0x3F));
+            o += (char)(0x80 | ((cp >> 6) & 0x3F));
+            o += (char)(0x80 | (cp & 0x3F));
+        }
+    }
+
+    uint32_t hex4() {
+        if (i + 4 > n) throw JsonError();
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) {
+            const int h = hexval(s[i + k]);
+            if (h < 0) throw JsonError();
+            v = (v << 4) | (uint32_t)h;
+        }
+        i += 4;
+        return v;
+    }
+
+    // A JSON string at s[i] ('"'): *p/*len = its UTF-8 text (in the input when it has no
+    // escapes, else in tmp).  Lone UTF-16 surrogates have no UTF-8 form: fallback.
+    void string(const char** p, uint64_t* len) {
+        expect('"');
+        const uint64_t b = i;
+        while (i < n && s[i] != '"' && s[i] != '\\') {
+            if ((uint8_t)s[i] < 0x20) throw JsonError();
+            ++i;
+        }
+        if (i >= n) throw JsonError();
+        if (s[i] == '"') {
+            *p = s + b;
+            *len = i - b;
+            ++i;
+            return;
+        }
+        tmp.assign(s + b, i - b);
+        while (true) {
+            if (i >= n) throw JsonError();
+            const char c = s[i];
+            if (c == '"') { ++i; break; }
+            if ((uint8_t)c < 0x20) throw JsonError();
+            if (c != '\\') { tmp += c; ++i; continue; }
+            if (++i >= n) throw JsonError();
+            const char e = s[i++];
+            switch (e) {
+                case '"': tmp += '"'; break;
+                case '\\': tmp += '\\'; break;
+                case '/': tmp += '/'; break;
+                case 'b': tmp += '\b'; break;
+                case 'f': tmp += '\f'; break;
+                case 'n': tmp += '\n'; break;
+                case 'r': tmp += '\r'; break;
+                case 't': tmp += '\t'; break;
+                case 'u': {
+                    uint32_t cp = hex4();
+                    if (cp >= 0xD800 && cp < 0xDC00) {
+                        if (i + 6 <= n && s[i] == '\\' && s[i + 1] == 'u') {
+                            i += 2;
+                            const uint32_t lo = hex4();
+                            if (lo < 0xDC00 || lo >= 0xE000) throw Fallback();
+                            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                        } else {
+                            throw Fallback();
+                        }
+                    } else if (cp >= 0xDC00 && cp < 0xE000) {
+                        throw Fallback();
+                    }
+                    put_utf8(tmp, cp);
+                    break;
+                }
+                default: throw JsonError();
+            }
+        }
+        *p = tmp.data();
+        *len = tmp.size();
+    }
+
+    void skip_string() {
+        expect('"');
+        while (true) {
+            if (i >= n) throw JsonError();
+            const char c = s[i];
+            if (c == '"') { ++i; return; }
+            if ((uint8_t)c < 0x20) throw JsonError();
+            if (c == '\\') {
+                if (++i >= n) throw JsonError();
+                const char e = s[i++];
+                if (e == 'u') {
+                    const uint32_t cp = hex4();
+                    // values are re-read by the caller's JSON decoder; lone surrogates
+                    // there are its business, but keep the fast path to well-formed text
+                    if (cp >= 0xD800 && cp < 0xE000) throw Fallback();
+                } else if (!strchr("\"\\/bfnrt", e)) {
+                    throw JsonError();
+                }
+            } else {
+                ++i;
+            }
+        }
+    }
+
+    void number() {
+        const uint64_t b = i;
+        if (peek() == '-') ++i;
+        if (i >= n) throw JsonError();
+        if (s[i] == '0') {
+            ++i;
+        } else if (s[i] >= '1' && s[i] <= '9') {
+            while (i < n && digit(s[i]) >= 0) ++i;
+        } else {
+            // NaN / Infinity: Python's json accepts them, Dart's does not — let the caller decide
+            if (s[i] == 'N' || s[i] == 'I') throw Fallback();
+            throw JsonError();
+        }
+        if (peek() == '.') {
+            ++i;
+            if (digit(peek()) < 0) throw JsonError();
+            while (i < n && digit(s[i]) >= 0) ++i;
+        }
+        if (peek() == 'e' || peek() == 'E') {
+            ++i;
+            if (peek() == '+' || peek() == '-') ++i;
+            if (digit(peek()) < 0) throw JsonError();
+            while (i < n && digit(s[i]) >= 0) ++i;
+        }
+        if (i == b) throw JsonError();
+    }
+
+    void literal(const char* w) {
+        const uint64_t l = strlen(w);
+        if (i + l > n || memcmp(s + i, w, l) != 0) throw JsonError();
+        i += l;
+    }
+
+    void skip_value(int depth) {
+        if (depth > 256) throw Fallback();
+        ws();
+        const char c = peek();
+        if (c == '{') {
+            ++i;
+            ws();
+            if (peek() == '}') { ++i; return; }
+            while (true) {
+                ws();
+                skip_string();
+                ws();
+                expect(':');
+                skip_value(depth + 1);
+                ws();
+                if (peek() == ',') { ++i; continue; }
+                expect('}');
+                return;
+            }
+        } else if (c == '[') {
+            ++i;
+            ws();
+            if (peek() == ']') { ++i; return; }
+            while (true) {
+                skip_value(depth + 1);
+                ws();
+                if (peek() == ',') { ++i; continue; }
+                expect(']');
+                return;
+            }
+        } else if (c == '"') {
+            skip_string();
+        } else if (c == 't') {
+            literal("true");
+        } else if (c == 'f') {
+            literal("false");
+        } else if (c == 'n') {
+            literal("null");
+        } else if (c == 'N' || c == 'I') {
+            throw Fallback();
+        } else {
+            number();
+        }
+    }
+};
+
+// Hlc.parse of the Hlc.toString form "YYYY-MM-DDTHH:MM:SS.mmmZ-XXXX-<node>" (hlc.dart:39-46:
+// counterDash = indexOf('-', lastIndexOf(':')), nodeIdDash = indexOf('-', counterDash + 1),
+// millis = DateTime.parse(..).millisecondsSinceEpoch, counter = int.parse(.., radix: 16)).
+// The fast form needs its last ':' at 16 (no ':' in the node id).
+bool parse_hlc(const char* t, uint64_t len, int64_t* lt, uint64_t* node_pos) {
+    if (len < 30) return false;
+    for (uint64_t k = 17; k < len; ++k)
+        if (t[k] == ':') return false;
+    static const char sep[24] = {0, 0, 0, 0, '-', 0, 0, '-', 0, 0, 'T', 0, 0, ':', 0, 0, ':', 0, 0, '.', 0, 0, 0, 'Z'};
+    int64_t v[24];
+    for (int k = 0; k < 24; ++k) {
+        if (sep[k]) {
+            if (t[k] != sep[k]) return false;
+        } else {
+            v[k] = digit(t[k]);
+            if (v[k] < 0) return false;
+        }
+    }
+    if (t[24] != '-' || t[29] != '-') return false;
+    int64_t counter = 0;
+    for (int k = 25; k < 29; ++k) {
+        const int h = hexval(t[k]);
+        if (h < 0) return false;
+        counter = (counter << 4) | h;
+    }
+    int64_t year = v[0] * 1000 + v[1] * 100 + v[2] * 10 + v[3];
+    const int64_t month = v[5] * 10 + v[6], day = v[8] * 10 + v[9];
+    const int64_t hour = v[11] * 10 + v[12], minute = v[14] * 10 + v[15], second = v[17] * 10 + v[18];
+    const int64_t milli = v[20] * 100 + v[21] * 10 + v[22];
+    // DateTime.parse normalises out-of-range fields (as crdt_amd/hlc.py::millis_from_iso)
+    int64_t mz = month - 1;
+    year += floordiv(mz, 12);
+    mz -= floordiv(mz, 12) * 12;
+    const int64_t days = days_from_civil(year, mz + 1, 1) + day - 1;
+    const int64_t ms = (((days * 24 + hour) * 60 + minute) * 60 + second) * 1000 + milli;
+    if (ms > kMaxMs || ms < -kMaxMs) return false;
+    // Hlc(millis, counter, nodeId): millis >= 2^48 would be microseconds — impossible here
+    *lt = (int64_t)(((uint64_t)ms << kShift) + (uint64_t)counter);
+    *node_pos = 30;
+    return true;
+}
+
+// Open-addressing set of key ids met in one document -> their record index.
+struct IdMap {
+    std::vector<uint64_t> s;   // (id + 1) << 32 | record
+    uint64_t mask = 0, used = 0;
+    void init(uint64_t want) {
+        uint64_t cap = 64;
+        while (cap < want * 2) cap <<= 1;
+        s.assign(cap, 0);
+        mask = cap - 1;
+        used = 0;
+    }
+    // returns the record index of id, or inserts rec and returns UINT32_MAX
+    uint32_t get_or_put(uint32_t id, uint32_t rec) {
+        if ((used + 1) * 2 > s.size()) {
+            std::vector<uint64_t> old;
+            old.swap(s);
+            init(old.size());
+            for (uint64_t e : old)
+                if (e) raw_put(e);
+        }
+        uint64_t h = ((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 20;
+        for (uint64_t k = h & mask;; k = (k + 1) & mask) {
+            const uint64_t e = s[k];
+            if (!e) {
+                s[k] = ((uint64_t)(id + 1) << 32) | rec;
+                ++used;
+                return UINT32_MAX;
+            }
+            if ((e >> 32) == (uint64_t)id + 1) return (uint32_t)e;
+        }
+    }
+    void raw_put(uint64_t e) {
+        const uint32_t id = (uint32_t)(e >> 32) - 1;
+        uint64_t h = ((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 20;
+        uint64_t k = h & mask;
+        while (s[k]) k = (k + 1) & mask;
+        s[k] = e;
+        ++used;
+    }
+};
+
+int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
+    Parser p{js, len, 0, std::string()};
+    const uint64_t n0 = keys->size();
+    std::unordered_map<std::string, uint32_t> node_ix;
+    IdMap seen;
+    seen.init(1024);
+    std::string kbuf;
+    try {
+        p.ws();
+        p.expect('{');
+        p.ws();
+        if (p.peek() == '}') {
+            ++p.i;
+        } else {
+            while (true) {
+                p.ws();
+                const char* kp;
+                uint64_t kl;
+                p.string(&kp, &kl);
+                kbuf.assign(kp, kl);                       // p.tmp is reused below
+                p.ws();
+                p.expect(':');
+                p.ws();
+                // the record object: {"hlc": <string>, "value": <any>, ...}; last duplicate wins
+                if (p.peek() != '{') throw Fallback();
+                ++p.i;
+                bool have_hlc = false;
+                int64_t lt = 0;
+                std::string node;
+                uint64_t voff = 0;
+                uint32_t vlen = 0;
+                p.ws();
+                if (p.peek() == '}') {
+                    ++p.i;
+                } else {
+                    while (true) {
+                        p.ws();
+                        const char* fp;
+                        uint64_t fl;
+                        p.string(&fp, &fl);
+                        const bool is_hlc = fl == 3 && memcmp(fp, "hlc", 3) == 0;
+                        const bool is_val = fl == 5 && memcmp(fp, "value", 5) == 0;
+                        p.ws();
+                        p.expect(':');
+                        p.ws();
+                        if (is_hlc) {
+                            if (p.peek() != '"') throw Fallback();
+                            const char* hp;
+                            uint64_t hl;
+                            p.string(&hp, &hl);
+                            uint64_t npos;
+                            if (!parse_hlc(hp, hl, &lt, &npos)) throw Fallback();
+                            node.assign(hp + npos, hl - npos);
+                            have_hlc = true;
+                        } else if (is_val) {
+                            const uint64_t b = p.i;
+                            p.skip_value(1);
+                            const bool is_null = p.i - b == 4 && memcmp(js + b, "null", 4) == 0;
+                            if (p.i - b >= (1ull << 32)) throw Fallback();
+                            voff = is_null ? 0 : b;
+                            vlen = is_null ? 0 : (uint32_t)(p.i - b);
+                        } else {
+                            p.skip_value(1);
+                        }
+                        p.ws();
+                        if (p.peek() == ',') { ++p.i; continue; }
+                        p.expect('}');
+                        break;
+                    }
+                }
+                if (!have_hlc) throw Fallback();           // Hlc.parse(null) throws
+                uint32_t nid;
+                auto it = node_ix.find(node);
+                if (it == node_ix.end()) {
+                    nid = (uint32_t)d->nodes.size();
+                    node_ix.emplace(node, nid);
+                    d->nodes.push_back(node);
+                } else {
+                    nid = it->second;
+                }
+                const uint64_t h = hash_bytes(kbuf.data(), kbuf.size());
+                uint32_t id;
+                if (!keys->find(kbuf.data(), kbuf.size(), h, &id)) {
+                    if (keys->size() >= 0xFFFFFFF0ull) throw Fallback();
+                    id = keys->add(kbuf.data(), kbuf.size(), h);
+                }
+                const uint32_t rec = (uint32_t)d->key.size();
+                const uint32_t prev = seen.get_or_put(id, rec);
+                if (prev != UINT32_MAX) {                  // repeated key: first position, last record
+                    d->lt[prev] = lt;
+                    d->node[prev] = nid;
+                    d->voff[prev] = voff;
+                    d->vlen[prev] = vlen;
+                } else {
+                    d->key.push_back(id);
+                    d->lt.push_back(lt);
+                    d->node.push_back(nid);
+                    d->voff.push_back(voff);
+                    d->vlen.push_back(vlen);
+                }
+                p.ws();
+                if (p.peek() == ',') { ++p.i; continue; }
+                p.expect('}');
+                break;
+            }
+        }
+        p.ws();
+        if (p.i != len) throw JsonError();
+    } catch (const Fallback&) {
+        crdt_keys_truncate(keys, n0);
+        return CRDT_HOST_FALLBACK;
+    } catch (const JsonError&) {
+        crdt_keys_truncate(keys, n0);
+        return CRDT_HOST_E_JSON;
+    } catch (const std::bad_alloc&) {
+        crdt_keys_truncate(keys, n0);
+        return CRDT_HOST_E_NOMEM;
+    }
+    return CRDT_HOST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdt_host_abi_version(void) { return CRDT_HOST_ABI_VERSION; }
+
+crdt_keys* crdt_keys_create(void) { return new (std::nothrow) crdt_keys(); }
+void crdt_keys_destroy(crdt_keys* k) { delete k; }
+uint64_t crdt_keys_size(const crdt_keys* k) { return k ? k->size() : 0; }
+
+int crdt_keys_find(const crdt_keys* k, const char* p, uint64_t n, uint32_t* id) {
+    if (!k || (!p && n) || !id) return CRDT_HOST_E_INVALID;
+    return k->find(p, n, hash_bytes(p, n), id) ? 0 : 1;
+}
+
+int crdt_keys_intern(crdt_keys* k, const char* p, uint64_t n, uint32_t* id, int* is_new) {
+    if (!k || (!p && n) || !id) return CRDT_HOST_E_INVALID;
+    const uint64_t h = hash_bytes(p, n);
+    try {
+        const bool found = k->find(p, n, h, id);
+        if (!found) {
+            if (k->size() >= 0xFFFFFFF0ull) return CRDT_HOST_E_NOMEM;
+            *id = k->add(p, n, h);
+        }
+        if (is_new) *is_new = found ? 0 : 1;
+    } catch (const std::bad_alloc&) {
+        return CRDT_HOST_E_NOMEM;
+    }
+    return CRDT_HOST_OK;
+}
+
+uint64_t crdt_keys_bytes(const crdt_keys* k, uint64_t first, uint64_t count) {
+    if (!k || first + count > k->size()) return 0;
+    return k->off[first + count] - k->off[first];
+}
+
+int crdt_keys_export(const crdt_keys* k, uint64_t first, uint64_t count, char* buf, uint64_t cap,
+                     uint64_t* offsets) {
+    if (!k || !offsets || first + count > k->size()) return CRDT_HOST_E_INVALID;
+    const uint64_t b = k->off[first], e = k->off[first + count];
+    if (e - b > cap || (!buf && e > b)) return CRDT_HOST_E_INVALID;
+    if (e > b) memcpy(buf, k->arena.data() + b, e - b);
+    for (uint64_t i = 0; i <= count; ++i) offsets[i] = k->off[first + i] - b;
+    return CRDT_HOST_OK;
+}
+
+int crdt_keys_truncate(crdt_keys* k, uint64_t n) {
+    if (!k) return CRDT_HOST_E_INVALID;
+    if (n >= k->size()) return CRDT_HOST_OK;
+    k->arena.resize(k->off[n]);
+    k->off.resize(n + 1);
+    k->hash.resize(n);
+    k->rebuild(n > 8 ? n : 8);
+    return CRDT_HOST_OK;
+}
+
+int crdt_keys_clear(crdt_keys* k) { return crdt_keys_truncate(k, 0); }
+
+int crdt_json_decode(const char* json, uint64_t len, crdt_keys* keys, crdt_decoded** out) {
+    if (!keys || !out || (!json && len)) return CRDT_HOST_E_INVALID;
+    *out = nullptr;
+    crdt_decoded* d = new (std::nothrow) crdt_decoded();
+    if (!d) return CRDT_HOST_E_NOMEM;
+    const int st = decode(json, len, keys, d);
+    if (st != CRDT_HOST_OK) {
+        delete d;
+        return st;
+    }
+    *out = d;
+    return CRDT_HOST_OK;
+}
+
+void crdt_decoded_free(crdt_decoded* d) { delete d; }
+uint64_t crdt_decoded_count(const crdt_decoded* d) { return d ? d->key.size() : 0; }
+uint32_t crdt_decoded_node_count(const crdt_decoded* d) { return d ? (uint32_t)d->nodes.size() : 0; }
+
+int crdt_decoded_columns(const crdt_decoded* d, uint32_t* key_id, int64_t* lt, uint32_t* node, uint64_t* val_off,
+                         uint32_t* val_len) {
+    if (!d) return CRDT_HOST_E_INVALID;
+    const size_t n = d->key.size();
+    if (key_id) memcpy(key_id, d->key.data(), n * 4);
+    if (lt) memcpy(lt, d->lt.data(), n * 8);
+    if (node) memcpy(node, d->node.data(), n * 4);
+    if (val_off) memcpy(val_off, d->voff.data(), n * 8);
+    if (val_len) memcpy(val_len, d->vlen.data(), n * 4);
+    return CRDT_HOST_OK;
+}
+
+uint64_t crdt_decoded_node_bytes(const crdt_decoded* d) {
+    uint64_t b = 0;
+    if (d)
+        for (const auto& s : d->nodes) b += s.size();
+    return b;
+}
+
+int crdt_decoded_nodes(const crdt_decoded* d, char* buf, uint64_t cap, uint64_t* offsets) {
+    if (!d || !offsets) return CRDT_HOST_E_INVALID;
+    uint64_t o = 0;
+    offsets[0] = 0;
+    for (size_t i = 0; i < d->nodes.size(); ++i) {
+        const std::string& s = d->nodes[i];
+        if (o + s.size() > cap) return CRDT_HOST_E_INVALID;
+        if (!s.empty()) memcpy(buf + o, s.data(), s.size());
+        o += s.size();
+        offsets[i + 1] = o;
+    }
+    return CRDT_HOST_OK;
+}
+
+int crdt_hlc_format(const int64_t* lt, const uint32_t* node, uint64_t n, const char* node_buf,
+                    const uint64_t* node_off, char* out, uint64_t cap, uint64_t* out_off) {
+    if ((!lt || !node || !node_off || !out_off) && n) return CRDT_HOST_E_INVALID;
+    static const char hx[] = "0123456789ABCDEF";
+    uint64_t o = 0;
+    out_off[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int64_t ms = lt[i] >> kShift;                 // Hlc.fromLogicalTime (hlc.dart:37)
+        const int64_t counter = lt[i] & 0xFFFF;
+        if (ms > kMaxMs || ms < -kMaxMs) return CRDT_HOST_FALLBACK;
+        const int64_t days = floordiv(ms, 86400000);
+        int64_t rem = ms - days * 86400000;
+        int64_t y, mo, d;
+        civil_from_days(days, &y, &mo, &d);
+        if (y < 0 || y > 9999) return CRDT_HOST_FALLBACK;   // Dart's +/-YYYYYY forms: Python path
+        const int64_t h = rem / 3600000;
+        rem -= h * 3600000;
+        const int64_t mi = rem / 60000;
+        rem -= mi * 60000;
+        const int64_t s = rem / 1000, milli = rem - s * 1000;
+        const uint64_t nb = node_off[node[i]], ne = node_off[node[i] + 1];
+        if (o + 30 + (ne - nb) > cap) return CRDT_HOST_E_INVALID;
+        char* q = out + o;
+        q[0] = '0' + y / 1000; q[1] = '0' + y / 100 % 10; q[2] = '0' + y / 10 % 10; q[3] = '0' + y % 10;
+        q[4] = '-'; q[5] = '0' + mo / 10; q[6] = '0' + mo % 10; q[7] = '-'; q[8] = '0' + d / 10; q[9] = '0' + d % 10;
+        q[10] = 'T'; q[11] = '0' + h / 10; q[12] = '0' + h % 10; q[13] = ':'; q[14] = '0' + mi / 10;
+        q[15] = '0' + mi % 10; q[16] = ':'; q[17] = '0' + s / 10; q[18] = '0' + s % 10; q[19] = '.';
+        q[20] = '0' + milli / 100; q[21] = '0' + milli / 10 % 10; q[22] = '0' + milli % 10; q[23] = 'Z';
+        q[24] = '-';
+        q[25] = hx[(counter >> 12) & 15]; q[26] = hx[(counter >> 8) & 15]; q[27] = hx[(counter >> 4) & 15];
+        q[28] = hx[counter & 15];
+        q[29] = '-';
+        if (ne > nb) memcpy(q + 30, node_buf + nb, ne - nb);
+        o += 30 + (ne - nb);
+        out_off[i + 1] = o;
+    }
+    return CRDT_HOST_OK;
+}
+
+}  // extern "C"

@@ -13,35 +13,76 @@ NULL_HANDLE = 0xFFFFFFFF
 
 class KeyIndex:
     """Key <-> dense id in first-committed order, so id order is the
-    LinkedHashMap insertion order of ``MapCrdt._map`` (map_crdt.dart:10)."""
+    LinkedHashMap insertion order of ``MapCrdt._map`` (map_crdt.dart:10).
+
+    String keys live in the native table of ``libcrdt_host.so`` (``hostlib.NativeKeys``),
+    which the native JSON decoder interns into directly; ``keys`` (id -> key) is filled
+    lazily from it.  The first non-string key (``MapCrdt<K, V>`` with any ``K``) moves the
+    index to a Python dict for good; so does a missing host library."""
 
     def __init__(self):
-        self.ids: dict = {}
-        self.keys: list = []
+        from . import hostlib
+        self._native = hostlib.NativeKeys() if hostlib.available() else None
+        self._ids: dict = {}
+        self._list: list = []
+
+    @property
+    def native(self):
+        """The native table while every key is a string, else None."""
+        return self._native
 
     def __len__(self):
-        return len(self.keys)
+        return len(self._native) if self._native is not None else len(self._list)
+
+    @property
+    def keys(self) -> list:
+        if self._native is not None and len(self._list) < len(self._native):
+            self._list.extend(self._native.export(len(self._list), len(self._native) - len(self._list)))
+        return self._list
+
+    def _to_python(self):
+        keys = self.keys
+        self._ids = {k: i for i, k in enumerate(keys)}
+        self._native = None
 
     def get(self, key):
-        return self.ids.get(key)
+        if self._native is not None:
+            if not isinstance(key, str):
+                return None
+            from .hostlib import utf8
+            return self._native.find(utf8(key))
+        return self._ids.get(key)
 
     def intern(self, key) -> int:
-        i = self.ids.get(key)
+        if self._native is not None:
+            if isinstance(key, str):
+                from .hostlib import utf8
+                i = self._native.intern(utf8(key))
+                if i == len(self._list):
+                    self._list.append(key)
+                return i
+            self._to_python()
+        i = self._ids.get(key)
         if i is None:
-            i = len(self.keys)
-            self.ids[key] = i
-            self.keys.append(key)
+            i = len(self._list)
+            self._ids[key] = i
+            self._list.append(key)
         return i
 
     def truncate(self, n: int):
         """Forget ids >= n (keys first seen in changesets that were not stored)."""
-        for k in self.keys[n:]:
-            del self.ids[k]
-        del self.keys[n:]
+        if self._native is not None:
+            self._native.truncate(n)
+        else:
+            for k in self._list[n:]:
+                del self._ids[k]
+        del self._list[n:]
 
     def clear(self):
-        self.ids.clear()
-        self.keys.clear()
+        if self._native is not None:
+            self._native.clear()
+        self._ids.clear()
+        self._list.clear()
 
 
 class NodeRanks:
@@ -60,6 +101,11 @@ class NodeRanks:
 
     def __len__(self):
         return len(self._nodes)
+
+    @property
+    def kind(self):
+        """'str' or 'int' once a node id is registered, else None."""
+        return self._kind
 
     def rank(self, node_id) -> int:
         return self._rank[node_id]
@@ -96,12 +142,20 @@ class NodeRanks:
         return [self._rank[n] for n in old_nodes]
 
 
+_RAW = object()            # handle whose value is still raw JSON text (decoded on first get)
+
+
 class ValueStore:
-    """Value <-> uint32 handle; ``None`` (tombstone) is ``NULL_HANDLE``."""
+    """Value <-> uint32 handle; ``None`` (tombstone) is ``NULL_HANDLE``.
+
+    ``put_raw`` registers a batch of JSON value spans (from the native decoder) without
+    building Python objects: such a value is ``json.loads``-ed on its first ``get``."""
 
     def __init__(self):
         self._values: list = []
         self._free: list = []
+        self._raw_start: list = []          # sorted first handles of raw batches
+        self._raw: list = []                # [buf, off, len, live] per batch (None when dropped)
 
     def __len__(self):
         return len(self._values) - len(self._free)
@@ -119,13 +173,57 @@ class ValueStore:
         self._values.append(value)
         return h
 
+    def put_raw(self, buf: bytes, off, length):
+        """Handles for the JSON texts buf[off[i] : off[i] + length[i]]; length 0 = null."""
+        import numpy as np
+        length = np.asarray(length)
+        out = np.full(len(length), NULL_HANDLE, np.uint32)
+        nz = np.flatnonzero(length)
+        m = len(nz)
+        if m == 0:
+            return out
+        h0 = len(self._values)
+        if h0 + m >= NULL_HANDLE:
+            raise MemoryError("value handle space exhausted")
+        self._values.extend([_RAW] * m)
+        self._raw_start.append(h0)
+        self._raw.append([buf, np.asarray(off)[nz].astype(np.int64), length[nz].astype(np.int64), m])
+        out[nz] = np.arange(h0, h0 + m, dtype=np.uint32)
+        return out
+
+    def _batch(self, h: int) -> int:
+        return bisect.bisect_right(self._raw_start, h) - 1
+
+    def _retire_raw(self, h: int):
+        b = self._raw[self._batch(h)]
+        b[3] -= 1
+        if b[3] == 0:                       # every value of the batch decoded or freed
+            b[0] = b[1] = b[2] = None
+
     def get(self, handle: int):
-        return None if handle == NULL_HANDLE else self._values[handle]
+        if handle == NULL_HANDLE:
+            return None
+        v = self._values[handle]
+        if v is _RAW:
+            import json
+            bi = self._batch(handle)
+            buf, off, ln, _ = self._raw[bi]
+            k = handle - self._raw_start[bi]
+            v = json.loads(buf[off[k]:off[k] + ln[k]])
+            self._values[handle] = v
+            self._retire_raw(handle)
+        return v
 
     def release(self, handle: int):
         if handle != NULL_HANDLE:
+            if self._values[handle] is _RAW:
+                self._retire_raw(handle)
             self._values[handle] = None
             self._free.append(handle)
+
+    def release_many(self, handles):
+        for h in handles:
+            self.release(int(h))
 
     def compact(self, live_handles):
         """Free every handle not in ``live_handles``."""
@@ -133,9 +231,10 @@ class ValueStore:
         free = set(self._free)
         for h in range(len(self._values)):
             if h not in live and h not in free:
-                self._values[h] = None
-                self._free.append(h)
+                self.release(h)
 
     def clear(self):
         self._values.clear()
         self._free.clear()
+        self._raw_start.clear()
+        self._raw.clear()

@@ -289,3 +289,107 @@ def _random_ops_vs_oracle(seed, n_ops=40):
 @pytest.mark.parametrize("seed", range(6))
 def test_random_operation_sequences(gpu_device, seed):
     _random_ops_vs_oracle(seed)
+
+
+# ------------------------------------------------------ native mergeJson ingest
+def _json_ops_vs_oracle(seed, n_ops=30, force_python=False):
+    """mergeJson through libcrdt_host.so (or the Python decoder) against the oracle's
+    merge_json: same state, same exceptions, same watch events."""
+    from oracle import crdt_oracle as O
+    rng = np.random.default_rng(seed)
+    nodes = ["local", "a", "m-x", "zz", "b0", "ü", ""]
+    dev, ora = MapCrdt("local"), O.MapCrdt("local")
+    if force_python:
+        dev._native_ingest = lambda: False
+    w = dev.watch()
+    wall = WALL
+    paths = set()
+    for _ in range(n_ops):
+        wall += int(rng.integers(0, 3))
+        if rng.random() < 0.25:
+            k, v = f"k{rng.integers(0, 30)}", int(rng.integers(0, 100))
+            e1 = e2 = None
+            try:
+                dev.put(k, v, wall=wall)
+            except Exception as ex:  # noqa: BLE001
+                e1 = type(ex).__name__
+            try:
+                ora.put(k, v, wall)
+            except Exception as ex:  # noqa: BLE001
+                e2 = type(ex).__name__
+            assert e1 == e2
+        else:
+            recs = {}
+            for k in rng.choice(40, int(rng.integers(0, 15)), replace=False):
+                ms = wall + int(rng.integers(-50, 8)) + (60001 if rng.random() < 0.01 else 0)
+                node = nodes[int(rng.integers(0, len(nodes)))] if rng.random() < 0.97 else "local"
+                val = None if rng.random() < 0.15 else [int(rng.integers(0, 1000)), {"s": "é"}]
+                recs[f"k{k}"] = O.Record(O.Hlc(ms, int(rng.integers(0, 3)), node), val, O.Hlc(0, 0, "local"))
+            doc = O.CrdtJson.encode(recs)
+            e1 = e2 = None
+            try:
+                dev.mergeJson(doc, wall=wall)
+            except Exception as ex:  # noqa: BLE001
+                e1 = (type(ex).__name__, str(ex))
+            paths.add(getattr(dev, "last_ingest", None))
+            try:
+                ora.merge_json(doc, wall)
+            except Exception as ex:  # noqa: BLE001
+                e2 = (type(ex).__name__, str(ex))
+            assert e1 == e2
+        rm_d, rm_o = dev.recordMap(), ora.record_map()
+        assert list(rm_d) == list(rm_o)
+        for k in rm_o:
+            assert rm_d[k].hlc.logicalTime == rm_o[k].hlc.logical_time
+            assert rm_d[k].hlc.nodeId == rm_o[k].hlc.node_id
+            assert rm_d[k].value == rm_o[k].value
+            assert rm_d[k].modified.logicalTime == rm_o[k].modified.logical_time
+        assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
+    assert [(k, v) for k, v in w] == list(ora.events)
+    return paths
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_merge_json_native_ingest_vs_oracle(gpu_device, seed):
+    assert _json_ops_vs_oracle(seed) == {"native"}
+
+
+def test_merge_json_python_decoder_vs_oracle(gpu_device):
+    assert _json_ops_vs_oracle(11, force_python=True) == {"python"}
+
+
+def _cfg1_docs(n_keys=10_000, seed=0xC0FFEE01):
+    """configs[0]: node_a local (putAll of every key, then a put per key), node_b's
+    10k-record JSON with 50 % key overlap; millis = base + U[0,2000), counter U[0,4)."""
+    from oracle import crdt_oracle as O
+    rng = np.random.default_rng(seed)
+    base = 1_735_689_600_000
+    keys = [f"k{i:05d}" for i in range(n_keys)]
+    remote_keys = keys[: n_keys // 2] + [f"k{i:05d}" for i in range(n_keys, n_keys + n_keys // 2)]
+    recs = {}
+    for k in remote_keys:
+        recs[k] = O.Record(O.Hlc(base + int(rng.integers(0, 2000)), int(rng.integers(0, 4)), "node_b"),
+                           int(rng.integers(0, 1 << 30)), O.Hlc(0, 0, "node_b"))
+    return base, keys, O.CrdtJson.encode(recs)
+
+
+def test_cfg1_merge_json_10k_keys_vs_oracle(gpu_device):
+    from oracle import crdt_oracle as O
+    base, keys, doc = _cfg1_docs()
+    dev, ora = MapCrdt("node_a"), O.MapCrdt("node_a")
+    dev.putAll({k: 0 for k in keys}, wall=base)
+    ora.put_all({k: 0 for k in keys}, base)
+    for i, k in enumerate(keys[::7]):
+        dev.put(k, i, wall=base + 1 + i % 1500)
+        ora.put(k, i, base + 1 + i % 1500)
+    wall = base + 10_000
+    dev.mergeJson(doc, wall=wall)
+    ora.merge_json(doc, wall)
+    assert dev.last_ingest == "native"
+    rm_d, rm_o = dev.recordMap(), ora.record_map()
+    assert list(rm_d) == list(rm_o) and len(rm_o) == 15_000
+    for k in rm_o:
+        assert (rm_d[k].hlc.logicalTime, rm_d[k].hlc.nodeId, rm_d[k].value, rm_d[k].modified.logicalTime) == \
+            (rm_o[k].hlc.logical_time, rm_o[k].hlc.node_id, rm_o[k].value, rm_o[k].modified.logical_time)
+    assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
+    assert dev.toJson() == ora.to_json()
