@@ -78,8 +78,8 @@ inline int hexval(char c) {
 struct crdt_keys {
     std::vector<char> arena;
     std::vector<uint64_t> off{0};      // off[id] .. off[id + 1]
-    std::vector<uint64_t> hash;        // per id
-    std::vector<uint32_t> slot;        // open addressing: id + 1, 0 = empty
+    std::vector<uint64_t> hash;        // per id (rebuilds)
+    std::vector<uint64_t> slot;        // open addressing: (hash >> 32) << 32 | (id + 1), 0 = empty
     uint64_t mask = 0;
 
     uint64_t size() const { return hash.size(); }
@@ -89,24 +89,37 @@ struct crdt_keys {
         while (cap < want * 2) cap <<= 1;
         slot.assign(cap, 0);
         mask = cap - 1;
-        for (uint64_t id = 0; id < hash.size(); ++id) {
-            uint64_t s = hash[id] & mask;
-            while (slot[s]) s = (s + 1) & mask;
-            slot[s] = (uint32_t)(id + 1);
-        }
+        for (uint64_t id = 0; id < hash.size(); ++id) place(hash[id], (uint32_t)id);
     }
 
+    void place(uint64_t h, uint32_t id) {
+        uint64_t s = h & mask;
+        while (slot[s]) s = (s + 1) & mask;
+        slot[s] = (h & 0xFFFFFFFF00000000ull) | (uint64_t)(id + 1);
+    }
+
+    // the slot word carries the hash's high half: a probe touches the key bytes only on a match
     bool find(const char* p, uint64_t n, uint64_t h, uint32_t* id) const {
         if (slot.empty()) return false;
+        const uint64_t hi = h & 0xFFFFFFFF00000000ull;
         for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-            const uint32_t v = slot[s];
+            const uint64_t v = slot[s];
             if (!v) return false;
-            const uint32_t i = v - 1;
-            if (hash[i] == h && off[i + 1] - off[i] == n && memcmp(arena.data() + off[i], p, n) == 0) {
+            if ((v & 0xFFFFFFFF00000000ull) != hi) continue;
+            const uint32_t i = (uint32_t)v - 1;
+            if (off[i + 1] - off[i] == n && memcmp(arena.data() + off[i], p, n) == 0) {
                 *id = i;
                 return true;
             }
         }
+    }
+
+    void reserve(uint64_t more_keys, uint64_t more_bytes) {
+        const uint64_t want = hash.size() + more_keys;
+        if (want * 2 > slot.size()) rebuild(want);
+        arena.reserve(arena.size() + more_bytes);
+        off.reserve(want + 1);
+        hash.reserve(want);
     }
 
     uint32_t add(const char* p, uint64_t n, uint64_t h) {
@@ -115,9 +128,7 @@ struct crdt_keys {
         arena.insert(arena.end(), p, p + n);
         off.push_back(arena.size());
         hash.push_back(h);
-        uint64_t s = h & mask;
-        while (slot[s]) s = (s + 1) & mask;
-        slot[s] = id + 1;
+        place(h, id);
         return id;
     }
 };
@@ -430,7 +441,13 @@ int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
     const uint64_t n0 = keys->size();
     std::unordered_map<std::string, uint32_t> node_ix;
     IdMap seen;
-    seen.init(1024);
+    const uint64_t est = len / 48 + 16;                  // a record is >= ~48 bytes of JSON
+    seen.init(est);
+    keys->reserve(est, len / 4);
+    d->key.reserve(est); d->lt.reserve(est); d->node.reserve(est); d->voff.reserve(est); d->vlen.reserve(est);
+    const char* last_node = nullptr;                    // records of one changeset mostly share a node
+    uint64_t last_len = 0;
+    uint32_t last_nid = 0;
     std::string kbuf;
     try {
         p.ws();
@@ -497,13 +514,20 @@ int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
                 }
                 if (!have_hlc) throw Fallback();           // Hlc.parse(null) throws
                 uint32_t nid;
-                auto it = node_ix.find(node);
-                if (it == node_ix.end()) {
-                    nid = (uint32_t)d->nodes.size();
-                    node_ix.emplace(node, nid);
-                    d->nodes.push_back(node);
+                if (last_node && node.size() == last_len && memcmp(node.data(), last_node, last_len) == 0) {
+                    nid = last_nid;
                 } else {
-                    nid = it->second;
+                    auto it = node_ix.find(node);
+                    if (it == node_ix.end()) {
+                        nid = (uint32_t)d->nodes.size();
+                        node_ix.emplace(node, nid);
+                        d->nodes.push_back(node);
+                    } else {
+                        nid = it->second;
+                    }
+                    last_node = d->nodes[nid].data();
+                    last_len = d->nodes[nid].size();
+                    last_nid = nid;
                 }
                 const uint64_t h = hash_bytes(kbuf.data(), kbuf.size());
                 uint32_t id;
