@@ -241,11 +241,21 @@ def main():
     alg_per_launch = kb / launches_per_step
     avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)                  # HIP events, sampled launches
     achieved = alg_per_launch / (avg_launch_us / 1e6) if apply_ms > 0 else 0.0
+    path = table.last_path()
     roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
-                "kernel": "k_apply (K2)", "avg_launch_us": round(avg_launch_us, 2),
+                "kernel": "k_apply (K2)" if path == "gather" else
+                "sorted apply: k_part_* x2 + k_resolve (one timed region per merge call)",
+                "avg_launch_us": round(avg_launch_us, 2),
                 "alg_bytes_per_launch": int(alg_per_launch), "launches_per_step": launches_per_step,
                 "launches_timed": apply_launches}
+    if path == "gather" and args.config == "fanin" and apply_ms > 0:
+        # K2 against the measured ceiling of its own access pattern: random 16-B row reads
+        # with 25 % of rows written back on a 2^28-row table (tools/ubench_rowwrite.hip)
+        rate = (n_owned / launches_per_step) / (avg_launch_us / 1e6)
+        roofline["pattern_ceiling"] = {"value": 30.4e9, "unit": "records/s", "achieved": round(rate, 1),
+                                       "frac": round(rate / 30.4e9, 3),
+                                       "source": "profiles/r01_ubench_rowwrite.txt"}
     # traffic (PMC) is filled from the committed rocprofv3 --pmc pass of this command, when present
     pmc = os.path.join(ROOT, "profiles", "pmc_k_apply.json")
     if os.path.exists(pmc) and world == 1 and args.config == "fanin":
@@ -288,7 +298,7 @@ def main():
         "scaling": "weak" if (world == 1 or weak) else "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
         "config": {"workload": workload, "records": total_records, "replicas": R,
                    "parallelism": (f"keyshard{world}-{'routed' if route else 'parts' if weak else 'home'}"
-                                   if world > 1 else "single"),
+                                   if world > 1 else "single"), "merge_path": path,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
