@@ -249,7 +249,7 @@ def main():
                 "avg_launch_us": round(avg_launch_us, 2),
                 "alg_bytes_per_launch": int(alg_per_launch), "launches_per_step": launches_per_step,
                 "launches_timed": apply_launches}
-    if path == "gather" and args.config == "fanin" and apply_ms > 0:
+    if path == "gather" and args.config == "fanin" and world == 1 and apply_ms > 0:
         # K2 against the measured ceiling of its own access pattern: random 16-B row reads
         # with 25 % of rows written back on a 2^28-row table (tools/ubench_rowwrite.hip)
         rate = (n_owned / launches_per_step) / (avg_launch_us / 1e6)
