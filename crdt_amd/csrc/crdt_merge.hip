@@ -41,7 +41,8 @@ constexpr int kApplyThreads = 256;
 // K2 records per thread (striped) are chosen per launch: 1, 2, 4 or 8
 constexpr int kCounterSlots = 64;                // striped n_present / n_won counters
 constexpr int kVerifyBlocks = 64;
-constexpr uint32_t kTimingStride = 16;          // time every 16th apply launch
+constexpr uint32_t kTimingStride = 32;          // every 32 apply launches, time a window of
+constexpr uint32_t kTimingWindow = 8;           // 8 back-to-back launches (one event pair)
 
 // Collective words are plain signed int64 so an RCCL MAX / MIN all-reduce combines them:
 //   maxima[j]  = M_j, INT64_MIN when changeset j is empty (or not homed here)
@@ -799,7 +800,7 @@ struct crdt_ctx {
     // timing
     bool timing = false;
     std::vector<hipEvent_t> events;
-    std::vector<uint32_t> launched;
+    std::vector<std::pair<uint32_t, uint32_t>> windows;   // timed (first changeset, launches)
     uint32_t apply_total = 0;
     // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
     int merge_path = 0;
@@ -1025,17 +1026,22 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
     }
     k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     ev_record(c, ev_base);
-    c->launched.clear();
+    c->windows.clear();
     uint32_t nl = 0;
     c->apply_total = 0;
+    int64_t win_j = -1;
+    uint32_t win_n = 0;
     for (uint32_t j = 0; j < R; ++j) {
         const uint64_t b = beg[j], e = fin[j];
         if (e == b) continue;
-        // HIP-event timing of a sample of the launches (every kTimingStride-th): per-launch
-        // durations without perturbing the rest of the stream
-        const bool timed = c->timing && (nl++ % kTimingStride) == 0;
+        // HIP-event timing of sampled windows of kTimingWindow back-to-back launches (one event
+        // pair per window, so the events do not split the stream the rest of the time)
+        if (c->timing && (nl++ % kTimingStride) == 0 && win_j < 0) {
+            win_j = j;
+            win_n = 0;
+            ev_record(c, ev_base + 1 + 2 * (size_t)j);
+        }
         c->apply_total++;
-        if (timed) { c->launched.push_back(j); ev_record(c, ev_base + 1 + 2 * (size_t)j); }
         // records per thread (measured: more gathers in flight per thread beats more
         // workgroups, down to ~100K records per changeset)
         const int items = c->apply_items ? c->apply_items : ((e - b) >= (512ull << 10) ? 4 : 2);
@@ -1052,7 +1058,15 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
         else
             k_apply<1><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
                                                               c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
-        if (timed) ev_record(c, ev_base + 2 + 2 * (size_t)j);
+        if (win_j >= 0 && ++win_n == kTimingWindow) {
+            ev_record(c, ev_base + 2 + 2 * (size_t)win_j);
+            c->windows.push_back({(uint32_t)win_j, win_n});
+            win_j = -1;
+        }
+    }
+    if (win_j >= 0) {
+        ev_record(c, ev_base + 2 + 2 * (size_t)win_j);
+        c->windows.push_back({(uint32_t)win_j, win_n});
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
@@ -1079,9 +1093,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
     const uint32_t R = c->plan_R;
     k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     ev_record(c, ev_base);
-    c->launched.clear();
+    c->windows.clear();
     c->apply_total = 1;
-    if (c->timing) { c->launched.push_back(0); ev_record(c, ev_base + 1); }
+    if (c->timing) { c->windows.push_back({0u, 1u}); ev_record(c, ev_base + 1); }
     const bool two = c->cap > (1ull << 20);
     const uint32_t shift1 = two ? 20u : (uint32_t)kSBits;
     for (uint32_t jb = 0; jb < R; jb += kWindow) {
@@ -1256,12 +1270,12 @@ void collect_timing(crdt_ctx* c, uint32_t R, bool full) {
         // events: 0 start, 1 after scan, 2 after clock/verify/resolve, 3 = apply base, then pairs
         if (hipEventElapsedTime(&ms, c->events[0], c->events[1]) == hipSuccess) t.scan_ms = ms;
         if (hipEventElapsedTime(&ms, c->events[1], c->events[2]) == hipSuccess) t.clock_ms = ms;
-        for (uint32_t j : c->launched) {
-            const size_t a = 4 + 2 * (size_t)j, b = a + 1;
+        for (const auto& w : c->windows) {
+            const size_t a = 4 + 2 * (size_t)w.first, b = a + 1;
             float d = 0;
             if (hipEventElapsedTime(&d, c->events[a], c->events[b]) == hipSuccess) {
                 t.apply_ms += d;
-                t.apply_launches++;
+                t.apply_launches += w.second;
             }
         }
         t.apply_total = c->apply_total;

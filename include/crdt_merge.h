@@ -91,8 +91,9 @@ typedef struct crdt_result {
 typedef struct crdt_timing {
     double scan_ms;            /* K3a: per-changeset max + candidate tiles */
     double clock_ms;           /* K3b/K3c: canonical prefix-max scan, exception resolution */
-    double apply_ms;           /* K2: summed durations of the SAMPLED apply launches (every 16th) */
-    uint32_t apply_launches;   /* how many apply launches were sampled */
+    double apply_ms;           /* K2: summed durations of SAMPLED windows of back-to-back apply launches
+                                  (8 launches every 32; the sorted path: its whole apply region) */
+    uint32_t apply_launches;   /* apply launches inside the sampled windows */
     uint32_t apply_total;      /* apply launches in the call */
     double total_ms;           /* first to last event of the call */
 } crdt_timing;
