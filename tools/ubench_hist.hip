@@ -11,6 +11,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#ifndef SHIFT_BITS
+#define SHIFT_BITS 20
+#endif
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 __device__ inline unsigned long long match_digit(uint32_t d, bool active) {
@@ -53,6 +56,34 @@ __global__ __launch_bounds__(T) void k_hist(const uint32_t* __restrict__ key, ui
         const unsigned long long m = match_digit(d, act);
         if (act && (m & below) == 0) atomicAdd(&h[d], (uint32_t)__popcll(m));
     }
+    __syncthreads();
+    for (int d = tid; d < 256; d += T) hist[(uint64_t)blockIdx.x * 256 + d] = h[d];
+}
+
+// G/H: one LDS atomic per key, no ballot aggregation (H returns the old value = a slot,
+// as a non-stable scatter would use it)
+template <int T, int Q, bool RET>
+__global__ __launch_bounds__(T) void k_hist_atomic(const uint32_t* __restrict__ key, uint64_t n,
+                                                   uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    const int tid = threadIdx.x;
+    for (int d = tid; d < 256; d += T) h[d] = 0;
+    const uint64_t beg = (uint64_t)blockIdx.x * T * Q;
+    uint32_t k[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint64_t i = beg + (uint64_t)q * T + tid;
+        k[q] = i < n ? __builtin_nontemporal_load(key + i) : 0u;
+    }
+    __syncthreads();
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t d = (k[q] >> SHIFT_BITS) & 255;
+        if (RET) acc += atomicAdd(&h[d], 1u);
+        else atomicAdd(&h[d], 1u);
+    }
+    if (RET && acc == 0x12345678u) hist[0] = acc;
     __syncthreads();
     for (int d = tid; d < 256; d += T) hist[(uint64_t)blockIdx.x * 256 + d] = h[d];
 }
@@ -123,7 +154,11 @@ int main() {
     float d = timeit([&] { k_hist<256, 32, true, true><<<n / 8192, 256>>>(key, n, hist); });
     float e = timeit([&] { k_hist4<1024, 8><<<n / 32768, 1024>>>((const u32x4*)key, n / 4, hist); });
     float f = timeit([&] { k_hist<256, 16, true, true><<<n / 4096, 256>>>(key, n, hist); });
+    float g = timeit([&] { k_hist_atomic<1024, 32, false><<<n / 32768, 1024>>>(key, n, hist); });
+    float h2 = timeit([&] { k_hist_atomic<1024, 32, true><<<n / 32768, 1024>>>(key, n, hist); });
+    // skewed digits: a third of the keys in digit 0 (the fan-in's level-1 shape)
     CK(hipGetLastError());
+    printf("G atomic/key %.3f ms (%.0f GB/s)  H atomic-with-return %.3f (%.0f)\n", g, gb / g * 1e3, h2, gb / h2 * 1e3);
     printf("1B keys (4.3 GB): A %.3f ms (%.0f GB/s)  B plain %.3f (%.0f)  C loads-only %.3f (%.0f)  "
            "D 256thr %.3f (%.0f)  E uint4 %.3f (%.0f)  F 256thr/16 %.3f (%.0f)\n",
            a, gb / a * 1e3, b, gb / b * 1e3, c, gb / c * 1e3, d, gb / d * 1e3, e, gb / e * 1e3, f, gb / f * 1e3);
