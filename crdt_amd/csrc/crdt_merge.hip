@@ -1144,9 +1144,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
-        k_part_scatter<true><<<nt1, kPThreads, 0, c->stream>>>(
-            cols.key, cols.lt, cols.rank, cols.val, nullptr, nullptr, tm1, jb, c->d_misc, c->cap, shift1,
-            c->p_toff.p, c->p1_rec.p, c->p1_kj.p);
+        k_part_scatter1<<<nt1, kPThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, tm1, jb,
+                                                           c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                                                           c->p1_kj.p);
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
