@@ -831,7 +831,6 @@ namespace {
     } while (0)
 
 inline unsigned grid_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
-inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 hipError_t ensure_events(crdt_ctx* c, size_t n) {
     while (c->events.size() < n) {
@@ -1164,9 +1163,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
             k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
-            k_part_scatter<false><<<nt2, kPThreads, 0, c->stream>>>(
-                nullptr, nullptr, nullptr, nullptr, c->p1_rec.p, c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
-                c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
+            k_part_scatter2<<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p,
+                                                               c->p2_rec.p, c->p2_kj.p);
         }
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
         const uint32_t nb = two ? kDigits * kDigits : kDigits;
