@@ -10,7 +10,7 @@ import os
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcrdt_mi355x.so")
+LIB_PATH = os.environ.get("CRDT_LIB_PATH") or os.path.join(_HERE, "libcrdt_mi355x.so")   # override: profiling builds
 
 CRDT_OK = 0
 CRDT_CLOCK_DRIFT = 1

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1194,6 +1195,18 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
     if (c->timing) ev_record(c, ev_base + 2);
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+#ifdef CRDT_PROF_RESOLVE
+    {
+        unsigned long long pr[8];
+        hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprof), sizeof(pr));
+        fprintf(stderr, "[rprof] items %llu chunks %llu | per item: init %.2f us final %.2f us | per chunk: "
+                "A %.2f us B %.2f us\n", pr[4], pr[5], pr[0] / 100.0 / (pr[4] ? pr[4] : 1),
+                pr[3] / 100.0 / (pr[4] ? pr[4] : 1), pr[1] / 100.0 / (pr[5] ? pr[5] : 1),
+                pr[2] / 100.0 / (pr[5] ? pr[5] : 1));
+        memset(pr, 0, sizeof(pr));
+        hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), pr, sizeof(pr));
+    }
+#endif
     crdt_result res = c->h_misc->result;
     uint64_t np = 0, nw_ = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw_ += c->h_misc->won[s]; }
