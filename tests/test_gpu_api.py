@@ -174,8 +174,18 @@ class TestMerge:                                     # map_crdt_test.dart:33-103
             c.merge({"y": Record(Hlc(WALL + 60001, 0, "q"), 2, hlc_now())})
         assert e.value.drift == 60001
 
+    def test_send_overflow_after_store(self, gpu_device):
+        """Hlc.send raises after putRecords (crdt.dart:90-93): the record stays stored and the
+        canonical stays at the received clock."""
+        c = crdt()
+        with pytest.raises(OverflowException) as e:
+            c.merge({"z": Record(Hlc(WALL, 0xFFFF, "q"), 3, hlc_now())}, wall=WALL)
+        assert e.value.counter == 0x10000
+        assert c.get("z") == 3
+        assert c.canonicalTime.logicalTime == (WALL << 16) + 0xFFFF
 
-class TestSerialization:                             # map_crdt_test.dart:105-201
+
+class TestSerialization:                            # map_crdt_test.dart:105-201
     def test_json_encode(self, gpu_device):
         hlcNow = hlc_now()
         c = crdt(seed={"x": Record(Hlc(MILLIS, 0, "abc"), 1, hlcNow)})

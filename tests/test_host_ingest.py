@@ -46,7 +46,7 @@ def _python_records(js):
     return {k: (r.hlc.logicalTime, r.hlc.nodeId, r.value) for k, r in m.items()}
 
 
-def _random_doc(rng, n, n_nodes=5, dup_frac=0.05, weird=False):
+def _random_doc(rng, n, n_nodes=5, dup_frac=0.05):
     nodes = [f"node-{i}" for i in range(n_nodes)] + ["", "a-b-c", "ünï-ñode", "漢字", "x y"]
     keys = []
     parts = []
