@@ -7,7 +7,8 @@
 //
 // Kernels (one HIP stream per ctx; every call is synchronous at the API edge):
 //   K3a k_scan     per-changeset max lt (M_j) + tiles holding a record that can
-//                  raise (Hlc.recv, hlc.dart:80-97)            [HBM stream, 12 B/record]
+//                  raise (Hlc.recv, hlc.dart:80-97)            [HBM stream, 8 B/record
+//                  + rank/millis only for records above C0]
 //   K3b k_clock    one workgroup: canonical recurrence C_j = send(max(C_{j-1}, M_j))
 //                  as a prefix max; R_j stamps; first send() failure (hlc.dart:51-74)
 //   K3c k_verify   exact first recv() failure inside candidate tiles (ordered
@@ -147,15 +148,21 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         const uint64_t base = beg + (uint64_t)t * kTile;
         int64_t m = INT64_MIN;
         int f = 0;
+        int64_t v[kScanItems];
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-            if (i < end) {
-                const int64_t v = lt[i];
-                const uint32_t r = rank[i];
-                const int64_t ms = millis ? millis[i] : (v >> kShift);
-                m = imax(m, v);
-                f |= (v > c0) & ((r == local_rank) | (wsub(ms, wall) > kMaxDrift));
+            v[q] = i < end ? lt[i] : INT64_MIN;
+            m = imax(m, v[q]);
+        }
+        // rank / millis matter only for records above C0 (the only ones recv() can raise on):
+        // a wave with none issues no load for them (the fan-in: ~all of them)
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            if (v[q] > c0) {
+                const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+                const int64_t ms = millis ? millis[i] : (v[q] >> kShift);
+                f |= (rank[i] == local_rank) | (wsub(ms, wall) > kMaxDrift);
             }
         }
         m = wave_max(m);
