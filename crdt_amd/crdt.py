@@ -232,6 +232,52 @@ class MapCrdt(Crdt):
         return {keys[int(i)]: self._make_record(int(i), lt[x], rank[x], val[x], mod[x])
                 for x, i in enumerate(ids)}
 
+    def toJson(self, modifiedSince: Hlc | None = None, keyEncoder=None, valueEncoder=None) -> str:
+        """crdt.dart:127-135 over recordMap (map_crdt.dart:42-45).  String keys and no encoders:
+        the rows come from the device compaction (crdt_modified_since) and the document is
+        assembled natively (hostlib.encode) — keys from the native table, Hlc.toString of the
+        columns, raw input values reused when already in dumps form — so no Record is built.
+        Anything else, or a Fallback from the native side, runs the restatement."""
+        if keyEncoder is None and valueEncoder is None and self._keys.native is not None:
+            from . import hostlib
+            try:
+                return self._native_export(modifiedSince)
+            except hostlib.Fallback:
+                pass
+        self.last_export = "python"
+        return super().toJson(modifiedSince, keyEncoder=keyEncoder, valueEncoder=valueEncoder)
+
+    def _native_export(self, modifiedSince: Hlc | None) -> str:
+        import json
+
+        from . import hostlib
+        from .crdt_json import _default
+        since = modifiedSince.logicalTime if modifiedSince is not None else 0
+        ids = self._table.modified_since(len(self._keys), since)
+        if len(ids) == 0:
+            self.last_export = "native"
+            return "{}"
+        lt, rank, val, _ = self._table.read_rows(ids)
+        hlc_text = None
+        if self._hlc_override:
+            pos = {int(k): x for x, k in enumerate(ids.tolist())} if len(self._hlc_override) > 64 else None
+            for kid, h in self._hlc_override.items():
+                row = pos.get(kid) if pos is not None else (
+                    int(np.searchsorted(ids, kid)) if kid <= int(ids[-1]) else None)
+                if row is not None and row < len(ids) and int(ids[row]) == kid:
+                    hlc_text = hlc_text or {}
+                    hlc_text[row] = str(h)
+
+        def dumps(objs):
+            return json.dumps(objs, separators=(",", ":"), ensure_ascii=False, default=_default)
+
+        ptr, ln, keep = self._values.texts(val, dumps)
+        nodes = [self._nodes.node(r) for r in range(len(self._nodes))]
+        out = hostlib.encode(self._keys.native, ids, lt, rank, nodes, ptr, ln, hlc_text)
+        del keep
+        self.last_export = "native"
+        return out
+
     def watch(self, key=None, **kw) -> Watch:                           # map_crdt.dart:47-49
         w = Watch(key, has_key=("key" in kw) or key is not None)
         self._watches.append(w)

@@ -8,6 +8,11 @@
 //                      CrdtJson.encode / Hlc.toString write (crdt_json.dart:8-17,
 //                      hlc.dart:101-104); everything else is CRDT_HOST_FALLBACK.
 //   * crdt_hlc_format  — Hlc.toString for a batch of clocks.
+//   * crdt_json_encode — the export half of sync: CrdtJson.encode (crdt_json.dart:8-17) of a
+//                      recordMap (map_crdt.dart:42-45) with Record.toJson (record.dart:28-31)
+//                      and Hlc.toJson = toString (hlc.dart:101-104, 122); value texts come
+//                      from the caller (crdt_json_canonical tells which raw input spans can
+//                      be reused verbatim, crdt_json_split cuts one dumped array into values).
 // Built with g++ -O3 (no GPU code).  Parity: tests/test_host_ingest.py compares every
 // column with the Python restatement (crdt_amd/crdt_json.py, crdt_amd/hlc.py).
 #include "crdt_host.h"
@@ -17,6 +22,8 @@
 
 #include <new>
 #include <string>
+#include <string_view>
+#include <unordered_set>
 #include <unordered_map>
 #include <vector>
 
@@ -572,6 +579,202 @@ int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
 
 }  // namespace
 
+
+namespace {
+
+// ------------------------------------------------------------------ export helpers
+// Hlc.toString's fixed 30-byte head "YYYY-MM-DDTHH:MM:SS.mmmZ-XXXX-" of Hlc.fromLogicalTime(lt)
+// (hlc.dart:37, 101-104); false outside years 0000..9999 (Dart's +/-YYYYYY forms).
+bool hlc_head(int64_t lt, char* q) {
+    static const char hx[] = "0123456789ABCDEF";
+    const int64_t ms = lt >> kShift;
+    const int64_t counter = lt & 0xFFFF;
+    if (ms > kMaxMs || ms < -kMaxMs) return false;
+    const int64_t days = floordiv(ms, 86400000);
+    int64_t rem = ms - days * 86400000;
+    int64_t y, mo, d;
+    civil_from_days(days, &y, &mo, &d);
+    if (y < 0 || y > 9999) return false;
+    const int64_t h = rem / 3600000;
+    rem -= h * 3600000;
+    const int64_t mi = rem / 60000;
+    rem -= mi * 60000;
+    const int64_t s = rem / 1000, milli = rem - s * 1000;
+    q[0] = '0' + y / 1000; q[1] = '0' + y / 100 % 10; q[2] = '0' + y / 10 % 10; q[3] = '0' + y % 10;
+    q[4] = '-'; q[5] = '0' + mo / 10; q[6] = '0' + mo % 10; q[7] = '-'; q[8] = '0' + d / 10; q[9] = '0' + d % 10;
+    q[10] = 'T'; q[11] = '0' + h / 10; q[12] = '0' + h % 10; q[13] = ':'; q[14] = '0' + mi / 10;
+    q[15] = '0' + mi % 10; q[16] = ':'; q[17] = '0' + s / 10; q[18] = '0' + s % 10; q[19] = '.';
+    q[20] = '0' + milli / 100; q[21] = '0' + milli / 10 % 10; q[22] = '0' + milli % 10; q[23] = 'Z';
+    q[24] = '-';
+    q[25] = hx[(counter >> 12) & 15]; q[26] = hx[(counter >> 8) & 15]; q[27] = hx[(counter >> 4) & 15];
+    q[28] = hx[counter & 15];
+    q[29] = '-';
+    return true;
+}
+
+// String body escaped as jsonEncode / json.dumps(ensure_ascii=False) write it: '"', '\\' and
+// the C0 controls (\b \t \n \f \r short, the rest \u00xx); every other byte verbatim.
+void json_escape(std::string& o, const char* p, uint64_t n) {
+    static const char hx[] = "0123456789abcdef";
+    uint64_t run = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint8_t c = (uint8_t)p[k];
+        if (c >= 0x20 && c != '"' && c != '\\') continue;
+        o.append(p + run, k - run);
+        run = k + 1;
+        switch (c) {
+            case '"': o += "\\\""; break;
+            case '\\': o += "\\\\"; break;
+            case '\b': o += "\\b"; break;
+            case '\t': o += "\\t"; break;
+            case '\n': o += "\\n"; break;
+            case '\f': o += "\\f"; break;
+            case '\r': o += "\\r"; break;
+            default: {
+                const char u[6] = {'\\', 'u', '0', '0', hx[c >> 4], hx[c & 15]};
+                o.append(u, 6);
+            }
+        }
+    }
+    o.append(p + run, n - run);
+}
+
+// Is text == json.dumps(json.loads(text), separators=(',', ':'), ensure_ascii=False)?  Then a
+// raw input span can be exported verbatim.  Conservative: any float, "-0", whitespace, an
+// escape dumps would not write, a repeated object key, a surrogate, invalid UTF-8 or a very
+// deep / very long number answers no (the caller then re-encodes that value).
+struct Canon {
+    const char* s;
+    uint64_t n, i = 0;
+
+    bool utf8_char() {                        // s[i] >= 0x80: one well-formed non-surrogate scalar
+        const uint8_t c = (uint8_t)s[i];
+        int len;
+        uint32_t cp;
+        if (c >= 0xC2 && c <= 0xDF) { len = 2; cp = c & 0x1F; }
+        else if (c >= 0xE0 && c <= 0xEF) { len = 3; cp = c & 0x0F; }
+        else if (c >= 0xF0 && c <= 0xF4) { len = 4; cp = c & 0x07; }
+        else return false;
+        if (i + len > n) return false;
+        for (int k = 1; k < len; ++k) {
+            const uint8_t t = (uint8_t)s[i + k];
+            if ((t & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (t & 0x3F);
+        }
+        if ((len == 3 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) || (len == 4 && (cp < 0x10000 || cp > 0x10FFFF)))
+            return false;
+        i += len;
+        return true;
+    }
+
+    bool string() {
+        if (i >= n || s[i] != '"') return false;
+        ++i;
+        while (i < n) {
+            const uint8_t c = (uint8_t)s[i];
+            if (c == '"') { ++i; return true; }
+            if (c < 0x20) return false;
+            if (c >= 0x80) {
+                if (!utf8_char()) return false;
+                continue;
+            }
+            if (c == '\\') {
+                if (i + 1 >= n) return false;
+                const char e = s[i + 1];
+                if (e == '"' || e == '\\' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't') {
+                    i += 2;
+                    continue;
+                }
+                // dumps writes \u00xx (lowercase) only for controls without a short form
+                if (e != 'u' || i + 6 > n || s[i + 2] != '0' || s[i + 3] != '0') return false;
+                const char a = s[i + 4], b = s[i + 5];
+                if (a != '0' && a != '1') return false;
+                if (!((b >= '0' && b <= '9') || (b >= 'a' && b <= 'f'))) return false;
+                const int v = (a - '0') * 16 + hexval(b);
+                if (v == 8 || v == 9 || v == 10 || v == 12 || v == 13) return false;
+                i += 6;
+                continue;
+            }
+            ++i;
+        }
+        return false;
+    }
+
+    bool number() {
+        const uint64_t b = i;
+        if (s[i] == '-') ++i;
+        if (i >= n) return false;
+        if (s[i] == '0') {
+            ++i;
+            if (i - b == 2) return false;             // "-0" loads as int 0
+        } else if (s[i] >= '1' && s[i] <= '9') {
+            while (i < n && s[i] >= '0' && s[i] <= '9') ++i;
+        } else {
+            return false;
+        }
+        if (i < n && (s[i] == '.' || s[i] == 'e' || s[i] == 'E')) return false;   // floats re-print
+        return i - b <= 4000;                         // Python's int string-length limit
+    }
+
+    bool lit(const char* w, uint64_t l) {
+        if (i + l > n || memcmp(s + i, w, l) != 0) return false;
+        i += l;
+        return true;
+    }
+
+    bool value(int depth) {
+        if (depth > 400 || i >= n) return false;
+        const char c = s[i];
+        if (c == '{') {
+            ++i;
+            if (i < n && s[i] == '}') { ++i; return true; }
+            std::vector<std::string_view> ks;
+            std::unordered_set<std::string_view> big;
+            while (true) {
+                const uint64_t kb = i;
+                if (!string()) return false;
+                const std::string_view k(s + kb, i - kb);     // canonical: equal bytes <=> equal keys
+                if (big.empty() && ks.size() < 16) {
+                    for (const auto& x : ks)
+                        if (x == k) return false;
+                    ks.push_back(k);
+                } else {
+                    if (big.empty()) big.insert(ks.begin(), ks.end());
+                    if (!big.insert(k).second) return false;
+                }
+                if (i >= n || s[i] != ':') return false;
+                ++i;
+                if (!value(depth + 1)) return false;
+                if (i < n && s[i] == ',') { ++i; continue; }
+                if (i < n && s[i] == '}') { ++i; return true; }
+                return false;
+            }
+        }
+        if (c == '[') {
+            ++i;
+            if (i < n && s[i] == ']') { ++i; return true; }
+            while (true) {
+                if (!value(depth + 1)) return false;
+                if (i < n && s[i] == ',') { ++i; continue; }
+                if (i < n && s[i] == ']') { ++i; return true; }
+                return false;
+            }
+        }
+        if (c == '"') return string();
+        if (c == 't') return lit("true", 4);
+        if (c == 'f') return lit("false", 5);
+        if (c == 'n') return lit("null", 4);
+        if (c == '-' || (c >= '0' && c <= '9')) return number();
+        return false;
+    }
+};
+
+}  // namespace
+
+struct crdt_text {
+    std::string s;
+};
+
 extern "C" {
 
 int crdt_host_abi_version(void) { return CRDT_HOST_ABI_VERSION; }
@@ -682,40 +885,113 @@ int crdt_decoded_nodes(const crdt_decoded* d, char* buf, uint64_t cap, uint64_t*
 int crdt_hlc_format(const int64_t* lt, const uint32_t* node, uint64_t n, const char* node_buf,
                     const uint64_t* node_off, char* out, uint64_t cap, uint64_t* out_off) {
     if ((!lt || !node || !node_off || !out_off) && n) return CRDT_HOST_E_INVALID;
-    static const char hx[] = "0123456789ABCDEF";
     uint64_t o = 0;
     out_off[0] = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        const int64_t ms = lt[i] >> kShift;                 // Hlc.fromLogicalTime (hlc.dart:37)
-        const int64_t counter = lt[i] & 0xFFFF;
-        if (ms > kMaxMs || ms < -kMaxMs) return CRDT_HOST_FALLBACK;
-        const int64_t days = floordiv(ms, 86400000);
-        int64_t rem = ms - days * 86400000;
-        int64_t y, mo, d;
-        civil_from_days(days, &y, &mo, &d);
-        if (y < 0 || y > 9999) return CRDT_HOST_FALLBACK;   // Dart's +/-YYYYYY forms: Python path
-        const int64_t h = rem / 3600000;
-        rem -= h * 3600000;
-        const int64_t mi = rem / 60000;
-        rem -= mi * 60000;
-        const int64_t s = rem / 1000, milli = rem - s * 1000;
         const uint64_t nb = node_off[node[i]], ne = node_off[node[i] + 1];
         if (o + 30 + (ne - nb) > cap) return CRDT_HOST_E_INVALID;
-        char* q = out + o;
-        q[0] = '0' + y / 1000; q[1] = '0' + y / 100 % 10; q[2] = '0' + y / 10 % 10; q[3] = '0' + y % 10;
-        q[4] = '-'; q[5] = '0' + mo / 10; q[6] = '0' + mo % 10; q[7] = '-'; q[8] = '0' + d / 10; q[9] = '0' + d % 10;
-        q[10] = 'T'; q[11] = '0' + h / 10; q[12] = '0' + h % 10; q[13] = ':'; q[14] = '0' + mi / 10;
-        q[15] = '0' + mi % 10; q[16] = ':'; q[17] = '0' + s / 10; q[18] = '0' + s % 10; q[19] = '.';
-        q[20] = '0' + milli / 100; q[21] = '0' + milli / 10 % 10; q[22] = '0' + milli % 10; q[23] = 'Z';
-        q[24] = '-';
-        q[25] = hx[(counter >> 12) & 15]; q[26] = hx[(counter >> 8) & 15]; q[27] = hx[(counter >> 4) & 15];
-        q[28] = hx[counter & 15];
-        q[29] = '-';
-        if (ne > nb) memcpy(q + 30, node_buf + nb, ne - nb);
+        if (!hlc_head(lt[i], out + o)) return CRDT_HOST_FALLBACK;
+        if (ne > nb) memcpy(out + o + 30, node_buf + nb, ne - nb);
         o += 30 + (ne - nb);
         out_off[i + 1] = o;
     }
     return CRDT_HOST_OK;
 }
+
+int crdt_json_canonical(const char* buf, const uint64_t* off, const uint32_t* len, uint64_t n, uint8_t* ok) {
+    if ((!buf || !off || !len || !ok) && n) return CRDT_HOST_E_INVALID;
+    try {
+        for (uint64_t k = 0; k < n; ++k) {
+            Canon c{buf + off[k], len[k]};
+            ok[k] = len[k] > 0 && c.value(0) && c.i == c.n;
+        }
+    } catch (const std::bad_alloc&) {
+        return CRDT_HOST_E_NOMEM;
+    }
+    return CRDT_HOST_OK;
+}
+
+int crdt_json_split(const char* json, uint64_t len, uint64_t count, uint64_t* off, uint32_t* elen) {
+    if ((!json && len) || ((!off || !elen) && count)) return CRDT_HOST_E_INVALID;
+    Parser p{json, len};
+    try {
+        p.expect('[');
+        uint64_t k = 0;
+        if (p.peek() == ']') {
+            ++p.i;
+        } else {
+            while (true) {
+                const uint64_t b = p.i;
+                p.skip_value(0);
+                if (k >= count || p.i - b > 0xFFFFFFFFull) return CRDT_HOST_FALLBACK;
+                off[k] = b;
+                elen[k] = (uint32_t)(p.i - b);
+                ++k;
+                if (p.peek() == ',') { ++p.i; continue; }
+                p.expect(']');
+                break;
+            }
+        }
+        if (k != count || p.i != len) return CRDT_HOST_FALLBACK;
+    } catch (const JsonError&) {
+        return CRDT_HOST_E_JSON;
+    } catch (const Fallback&) {
+        return CRDT_HOST_FALLBACK;
+    }
+    return CRDT_HOST_OK;
+}
+
+int crdt_json_encode(const crdt_keys* keys, const uint32_t* key_id, const int64_t* lt, const uint32_t* node,
+                     const char* const* hlc_txt, const uint32_t* hlc_len, const char* const* val_txt,
+                     const uint32_t* val_len, uint64_t n, const char* node_buf, const uint64_t* node_off,
+                     uint32_t n_nodes, crdt_text** out) {
+    if (!keys || !out || ((!key_id || !lt || !node || !val_len || !node_off) && n)) return CRDT_HOST_E_INVALID;
+    *out = nullptr;
+    crdt_text* t = new (std::nothrow) crdt_text();
+    if (!t) return CRDT_HOST_E_NOMEM;
+    try {
+        std::string& o = t->s;
+        uint64_t want = 2;
+        for (uint64_t i = 0; i < n; ++i) want += 64 + val_len[i];
+        o.reserve(want + want / 8);
+        o += '{';
+        char head[30];
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t id = key_id[i];
+            if (id >= keys->size() || node[i] >= n_nodes || (val_len[i] && (!val_txt || !val_txt[i]))) {
+                delete t;
+                return CRDT_HOST_E_INVALID;
+            }
+            if (i) o += ',';
+            o += '"';
+            json_escape(o, keys->arena.data() + keys->off[id], keys->off[id + 1] - keys->off[id]);
+            o += "\":{\"hlc\":\"";
+            if (hlc_txt && hlc_txt[i]) {                    // an Hlc not in columnar form (caller-made)
+                json_escape(o, hlc_txt[i], hlc_len[i]);
+            } else {
+                if (!hlc_head(lt[i], head)) {
+                    delete t;
+                    return CRDT_HOST_FALLBACK;
+                }
+                o.append(head, 30);
+                json_escape(o, node_buf + node_off[node[i]], node_off[node[i] + 1] - node_off[node[i]]);
+            }
+            o += "\",\"value\":";
+            if (val_len[i]) o.append(val_txt[i], val_len[i]);
+            else o += "null";
+            o += '}';
+        }
+        o += '}';
+    } catch (const std::bad_alloc&) {
+        delete t;
+        return CRDT_HOST_E_NOMEM;
+    }
+    *out = t;
+    return CRDT_HOST_OK;
+}
+
+const char* crdt_text_data(const crdt_text* t) { return t ? t->s.data() : nullptr; }
+uint64_t crdt_text_size(const crdt_text* t) { return t ? t->s.size() : 0; }
+void crdt_text_free(crdt_text* t) { delete t; }
 
 }  // extern "C"

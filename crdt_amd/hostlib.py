@@ -1,7 +1,7 @@
 """ctypes binding of ``include/crdt_host.h`` (``crdt_amd/libcrdt_host.so``).
 
-The native host ingest: key interning, ``CrdtJson.decode`` of the wire format into
-integer columns, and batch ``Hlc.toString``.  CPU code (g++), no GPU.  It decodes
+The native host half of sync: key interning, ``CrdtJson.decode`` of the wire format into
+integer columns, batch ``Hlc.toString``, and ``CrdtJson.encode`` of a record map (export).  CPU code (g++), no GPU.  It decodes
 the format the reference writes; for anything else it answers ``Fallback`` and the
 caller uses the Python restatement (``crdt_json.py`` / ``hlc.py``), so results do not
 depend on which decoder ran.
@@ -42,6 +42,12 @@ SIGNATURES = {
     "crdt_decoded_node_bytes": (_U64, [_P]),
     "crdt_decoded_nodes": (_INT, [_P, _P, _U64, _P]),
     "crdt_hlc_format": (_INT, [_P, _P, _U64, _P, _P, _P, _U64, _P]),
+    "crdt_json_encode": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U32, _P]),
+    "crdt_text_data": (_P, [_P]),
+    "crdt_text_size": (_U64, [_P]),
+    "crdt_text_free": (None, [_P]),
+    "crdt_json_canonical": (_INT, [_P, _P, _P, _U64, _P]),
+    "crdt_json_split": (_INT, [_P, _U64, _U64, _P, _P]),
 }
 
 
@@ -198,3 +204,75 @@ def hlc_strings(lt: np.ndarray, node: np.ndarray, node_ids: list) -> list:
     raw = out.raw[:int(ooffs[-1])]
     o = ooffs.tolist()
     return [raw[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(n)]
+
+
+def address(b: bytes) -> int:
+    """Address of a bytes object's buffer (valid while the object lives)."""
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value or 0
+
+
+def canonical(buf: bytes, off: np.ndarray, length: np.ndarray) -> np.ndarray:
+    """uint8 flags: span k of buf is what json.dumps(json.loads(span)) writes (exportable as is)."""
+    lib = load()
+    off = np.ascontiguousarray(off, np.uint64)
+    length = np.ascontiguousarray(length, np.uint32)
+    ok = np.zeros(len(off), np.uint8)
+    if len(off):
+        st = lib.crdt_json_canonical(buf, _ptr(off), _ptr(length), len(off), _ptr(ok))
+        if st != OK:
+            raise RuntimeError(f"crdt_json_canonical: {st}")
+    return ok
+
+
+def split_array(text: bytes, count: int):
+    """(off, len) of the ``count`` elements of the JSON array ``text``; raises Fallback."""
+    lib = load()
+    off = np.zeros(count, np.uint64)
+    ln = np.zeros(count, np.uint32)
+    st = lib.crdt_json_split(text, len(text), count, _ptr(off), _ptr(ln))
+    if st == FALLBACK:
+        raise Fallback("split")
+    if st != OK:
+        raise RuntimeError(f"crdt_json_split: {st}")
+    return off, ln
+
+
+def encode(keys: NativeKeys, key_id, lt, node, node_ids: list, val_ptr, val_len, hlc_text: dict | None = None) -> str:
+    """``CrdtJson.encode`` of rows (key_id, Hlc.fromLogicalTime(lt, node_ids[node]), value text at
+    val_ptr / val_len, 0 = null); ``hlc_text`` {row: str} overrides a row's hlc.  Raises Fallback
+    for years outside 0000..9999."""
+    lib = load()
+    n = len(key_id)
+    key_id = np.ascontiguousarray(key_id, np.uint32)
+    lt = np.ascontiguousarray(lt, np.int64)
+    node = np.ascontiguousarray(node, np.uint32)
+    val_ptr = np.ascontiguousarray(val_ptr, np.uint64)
+    val_len = np.ascontiguousarray(val_len, np.uint32)
+    enc = [utf8(str(x)) for x in node_ids]
+    nbuf = b"".join(enc) or b"\0"
+    noffs = np.zeros(len(enc) + 1, np.uint64)
+    np.cumsum([len(e) for e in enc], out=noffs[1:])
+    keep = []
+    hp = hl = None
+    if hlc_text:
+        hp = np.zeros(n, np.uint64)
+        hl = np.zeros(n, np.uint32)
+        for row, txt in hlc_text.items():
+            b = utf8(txt)
+            keep.append(b)
+            hp[row] = address(b)
+            hl[row] = len(b)
+    out = ctypes.c_void_p(None)
+    st = lib.crdt_json_encode(keys._h, _ptr(key_id), _ptr(lt), _ptr(node), _ptr(hp) if hp is not None else None,
+                              _ptr(hl) if hl is not None else None, _ptr(val_ptr), _ptr(val_len), n, nbuf,
+                              _ptr(noffs), len(enc), ctypes.byref(out))
+    if st == FALLBACK:
+        raise Fallback("year")
+    if st != OK:
+        raise RuntimeError(f"crdt_json_encode: {st}")
+    t = out.value
+    try:
+        raw = ctypes.string_at(lib.crdt_text_data(t), int(lib.crdt_text_size(t)))
+    finally:
+        lib.crdt_text_free(t)
+    return raw.decode("utf-8", "surrogatepass")

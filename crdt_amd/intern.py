@@ -149,13 +149,15 @@ class ValueStore:
     """Value <-> uint32 handle; ``None`` (tombstone) is ``NULL_HANDLE``.
 
     ``put_raw`` registers a batch of JSON value spans (from the native decoder) without
-    building Python objects: such a value is ``json.loads``-ed on its first ``get``."""
+    building Python objects: such a value is ``json.loads``-ed on its first ``get``, and
+    ``texts`` exports it without ever decoding it when its span is already in dumps form."""
 
     def __init__(self):
         self._values: list = []
         self._free: list = []
+        self._rawflag = bytearray()         # per handle: 1 = still raw JSON text
         self._raw_start: list = []          # sorted first handles of raw batches
-        self._raw: list = []                # [buf, off, len, live] per batch (None when dropped)
+        self._raw: list = []                # [buf, off, len, live, canonical flags] per batch
 
     def __len__(self):
         return len(self._values) - len(self._free)
@@ -166,11 +168,13 @@ class ValueStore:
         if self._free:
             h = self._free.pop()
             self._values[h] = value
+            self._rawflag[h] = 0
             return h
         h = len(self._values)
         if h >= NULL_HANDLE:
             raise MemoryError("value handle space exhausted")
         self._values.append(value)
+        self._rawflag.append(0)
         return h
 
     def put_raw(self, buf: bytes, off, length):
@@ -186,8 +190,9 @@ class ValueStore:
         if h0 + m >= NULL_HANDLE:
             raise MemoryError("value handle space exhausted")
         self._values.extend([_RAW] * m)
+        self._rawflag.extend(b"\x01" * m)
         self._raw_start.append(h0)
-        self._raw.append([buf, np.asarray(off)[nz].astype(np.int64), length[nz].astype(np.int64), m])
+        self._raw.append([buf, np.asarray(off)[nz].astype(np.int64), length[nz].astype(np.int64), m, None])
         out[nz] = np.arange(h0, h0 + m, dtype=np.uint32)
         return out
 
@@ -207,10 +212,11 @@ class ValueStore:
         if v is _RAW:
             import json
             bi = self._batch(handle)
-            buf, off, ln, _ = self._raw[bi]
+            buf, off, ln = self._raw[bi][:3]
             k = handle - self._raw_start[bi]
             v = json.loads(buf[off[k]:off[k] + ln[k]])
             self._values[handle] = v
+            self._rawflag[handle] = 0
             self._retire_raw(handle)
         return v
 
@@ -219,6 +225,7 @@ class ValueStore:
             if self._values[handle] is _RAW:
                 self._retire_raw(handle)
             self._values[handle] = None
+            self._rawflag[handle] = 0
             self._free.append(handle)
 
     def release_many(self, handles):
@@ -236,5 +243,56 @@ class ValueStore:
     def clear(self):
         self._values.clear()
         self._free.clear()
+        self._rawflag.clear()
         self._raw_start.clear()
         self._raw.clear()
+
+    def texts(self, handles, dumps):
+        """JSON texts of the values of ``handles`` for the native encoder: (ptr, len, keepalive).
+
+        A still-raw value whose input span is already what ``dumps`` writes is passed as that
+        span (never decoded); every other value is encoded by one ``dumps`` of the list of them,
+        which the native splitter cuts into elements.  len 0 = null (tombstone).  Raises
+        ``hostlib.Fallback`` when that list does not split (NaN / Infinity ...)."""
+        import numpy as np
+        from . import hostlib
+        h = np.asarray(handles, np.uint32)
+        n = len(h)
+        ptr = np.zeros(n, np.uint64)
+        ln = np.zeros(n, np.uint32)
+        keep = []
+        rows = np.flatnonzero(h != NULL_HANDLE)
+        if len(rows) == 0:
+            return ptr, ln, keep
+        hv = h[rows].astype(np.int64)
+        raw = np.frombuffer(bytes(self._rawflag), np.uint8)[hv].astype(bool)
+        other = rows[~raw]
+        if raw.any():
+            rr, rh = rows[raw], hv[raw]
+            starts = np.asarray(self._raw_start, np.int64)
+            bi = np.searchsorted(starts, rh, side="right") - 1
+            slow = []
+            for b in np.unique(bi):
+                sel = bi == b
+                batch = self._raw[int(b)]
+                buf, boff, blen = batch[0], batch[1], batch[2]
+                if batch[4] is None:                        # canonical flags, once per batch
+                    batch[4] = hostlib.canonical(buf, boff, blen).astype(bool)
+                k = rh[sel] - int(starts[b])
+                good = batch[4][k]
+                base = hostlib.address(buf)
+                keep.append(buf)
+                ptr[rr[sel][good]] = base + boff[k[good]].astype(np.uint64)
+                ln[rr[sel][good]] = blen[k[good]].astype(np.uint32)
+                slow.append(rr[sel][~good])
+            if slow:
+                other = np.sort(np.concatenate([other] + slow))
+        if len(other):
+            objs = [self.get(int(x)) for x in h[other]]
+            text = dumps(objs).encode("utf-8", "surrogatepass")
+            off, el = hostlib.split_array(text, len(objs))
+            keep.append(text)
+            ptr[other] = hostlib.address(text) + off
+            ln[other] = el
+            # a value that dumps to nothing cannot exist; length 0 stays reserved for null
+        return ptr, ln, keep

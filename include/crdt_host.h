@@ -1,4 +1,4 @@
-/* crdt_host.h — C-ABI of the native host ingest for the MapCrdt merge path.
+/* crdt_host.h — C-ABI of the native host ingest and export for the MapCrdt merge path.
  *
  * The north star keeps JSON decoding and string interning on the host; this
  * library is that host half, in C++ (crdt_amd/csrc/crdt_host.cpp, built with g++
@@ -6,7 +6,10 @@
  * format, the per-record work of
  *   Crdt.mergeJson -> CrdtJson.decode -> Record.fromJson -> Hlc.parse
  *   (crdt.dart:100-109, crdt_json.dart:19-37, record.dart:21-26, hlc.dart:39-46)
- * and produces the integer columns crdt_merge (crdt_merge.h) consumes.
+ * and produces the integer columns crdt_merge (crdt_merge.h) consumes; on the way out it
+ * replaces Crdt.toJson -> CrdtJson.encode -> Record.toJson -> Hlc.toString
+ * (crdt.dart:127-135, crdt_json.dart:8-17, record.dart:28-31, hlc.dart:101-104) for the rows
+ * crdt_modified_since selects (crdt_json_encode).
  *
  * Fast path = what CrdtJson.encode / Hlc.toString emit (crdt_json.dart:8-17,
  * hlc.dart:101-104): {"<key>": {"hlc": "YYYY-MM-DDTHH:MM:SS.mmmZ-XXXX-<node>",
@@ -24,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CRDT_HOST_ABI_VERSION 1
+#define CRDT_HOST_ABI_VERSION 2
 
 enum crdt_host_status {
     CRDT_HOST_OK = 0,
@@ -77,6 +80,35 @@ int crdt_decoded_nodes(const crdt_decoded* d, char* buf, uint64_t cap, uint64_t*
  * CRDT_HOST_FALLBACK if some millis is outside years 0000..9999. */
 int crdt_hlc_format(const int64_t* lt, const uint32_t* node, uint64_t n, const char* node_buf,
                     const uint64_t* node_off, char* out, uint64_t cap, uint64_t* out_off);
+
+/* ---- export: CrdtJson.encode (crdt_json.dart:8-17) of a recordMap (map_crdt.dart:42-45), one
+ * record per row in the given order:
+ *   {"<key>":{"hlc":"<Hlc.toString>","value":<value JSON>},...}
+ * (Record.toJson, record.dart:28-31; Hlc.toJson = toString, hlc.dart:101-104, 122).  Key i is
+ * key_id[i] of `keys`; its hlc is Hlc.fromLogicalTime(lt[i], node table entry node[i]) unless
+ * hlc_txt (optional) gives a preformatted text for row i (non-NULL entry); its value is the JSON
+ * text val_txt[i][0, val_len[i]) emitted as is (val_len 0 = null, a tombstone).  Keys, node ids
+ * and hlc texts are escaped as jsonEncode / json.dumps(ensure_ascii=False) do.  The document is
+ * returned in *out (crdt_text_*).  CRDT_HOST_FALLBACK: a millis outside years 0000..9999. */
+typedef struct crdt_text crdt_text;
+int crdt_json_encode(const crdt_keys* keys, const uint32_t* key_id, const int64_t* lt, const uint32_t* node,
+                     const char* const* hlc_txt, const uint32_t* hlc_len, const char* const* val_txt,
+                     const uint32_t* val_len, uint64_t n, const char* node_buf, const uint64_t* node_off,
+                     uint32_t n_nodes, crdt_text** out);
+const char* crdt_text_data(const crdt_text* t);
+uint64_t crdt_text_size(const crdt_text* t);
+void crdt_text_free(crdt_text* t);
+
+/* ok[k] = 1 when the JSON text buf[off[k], off[k] + len[k]) is exactly what
+ * json.dumps(json.loads(text), separators=(',', ':'), ensure_ascii=False) writes back, so a
+ * value decoded by crdt_json_decode can be exported verbatim (conservative: floats, "-0",
+ * whitespace, escapes dumps would not write, repeated object keys, surrogates answer 0). */
+int crdt_json_canonical(const char* buf, const uint64_t* off, const uint32_t* len, uint64_t n, uint8_t* ok);
+
+/* Spans (off, elen) of the `count` elements of one JSON array text (e.g. the values of a batch
+ * dumped at once).  CRDT_HOST_FALLBACK when it holds another number of elements or NaN /
+ * Infinity / lone surrogates; CRDT_HOST_E_JSON when malformed. */
+int crdt_json_split(const char* json, uint64_t len, uint64_t count, uint64_t* off, uint32_t* elen);
 
 #ifdef __cplusplus
 }

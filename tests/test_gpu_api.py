@@ -356,6 +356,11 @@ def _json_ops_vs_oracle(seed, n_ops=30, force_python=False):
             assert rm_d[k].modified.logicalTime == rm_o[k].modified.logical_time
         assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
     assert [(k, v) for k, v in w] == list(ora.events)
+    # export: native toJson (device compaction + libcrdt_host encode) == the oracle's
+    for since in (None, O.Hlc(WALL + 3, 0, "local"), O.Hlc(wall + 50, 0, "local")):
+        mine = None if since is None else Hlc(since.millis, since.counter, since.node_id)
+        assert dev.toJson(modifiedSince=mine) == ora.to_json(modified_since=since)
+        assert dev.last_export == "native"
     return paths
 
 
@@ -403,3 +408,44 @@ def test_cfg1_merge_json_10k_keys_vs_oracle(gpu_device):
             (rm_o[k].hlc.logical_time, rm_o[k].hlc.node_id, rm_o[k].value, rm_o[k].modified.logical_time)
     assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
     assert dev.toJson() == ora.to_json()
+
+
+# ------------------------------------------------------------ native toJson export
+def test_to_json_native_export_vs_restatement(gpu_device):
+    """MapCrdt.toJson through crdt_modified_since + crdt_json_encode against the Python
+    restatement (Crdt.toJson over recordMap): raw mergeJson values kept verbatim or re-encoded
+    (whitespace, floats, escapes, repeated keys), put() values, tombstones, escaped keys and
+    node ids, an Hlc outside the columnar form, modifiedSince."""
+    from crdt_amd.crdt import Crdt
+    c = MapCrdt("lo\"cal")
+    c.put("plain", {"a": [1, 2, None]}, wall=WALL)
+    c.put("flt", 1.5, wall=WALL)
+    c.put("tab\tkey", "é\n", wall=WALL)
+    c.putRecord("odd", Record(Hlc(WALL, 0x1FFFF, "z"), 3, Hlc(WALL, 0, "lo\"cal")))   # counter > 0xFFFF
+    texts = ['{"a":1}', '{"a": 1}', '1.0', '"\\u00e9"', '{"k":1,"k":2}', 'null', '[true,false]', '-0', '1e3',
+             '12345678901234567890']
+    doc = "{" + ",".join(f'"r{i}":{{"hlc":"{Hlc(WALL + 1, i, "n" + str(i % 3))}","value":{t}}}'
+                         for i, t in enumerate(texts)) + "}"
+    c.mergeJson(doc, wall=WALL + 1)
+    assert c.last_ingest == "native"
+    c.mergeJson('{"sur":{"hlc":"%s","value":"\\ud83d\\ude00"}}' % Hlc(WALL + 1, 0, "n"), wall=WALL + 1)
+    c.delete("plain", wall=WALL + 2)
+    for since in (None, Hlc(WALL + 1, 0, "x"), Hlc(WALL + 2, 0, "x"), Hlc(WALL + 9, 0, "x")):
+        want = Crdt.toJson(c, modifiedSince=since)
+        got = c.toJson(modifiedSince=since)
+        assert c.last_export == "native"
+        assert got == want, (since, got, want)
+    assert json.loads(c.toJson())["r3"]["value"] == "é"
+
+
+def test_to_json_encoders_and_int_keys_take_restatement(gpu_device):
+    c = MapCrdt("a")
+    c.put(7, "x", wall=WALL)
+    assert c.toJson() == f'{{"7":{{"hlc":"{Hlc(WALL, 0, "a")}","value":"x"}}}}'
+    assert c.last_export == "python"
+    s = MapCrdt("a")
+    s.put("k", 1, wall=WALL)
+    assert s.toJson(valueEncoder=lambda k, v: v + 1) == f'{{"k":{{"hlc":"{Hlc(WALL, 0, "a")}","value":2}}}}'
+    assert s.last_export == "python"
+    assert s.toJson() == f'{{"k":{{"hlc":"{Hlc(WALL, 0, "a")}","value":1}}}}'
+    assert s.last_export == "native"

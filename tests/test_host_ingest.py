@@ -24,11 +24,11 @@ pytestmark = pytest.mark.skipif(not hostlib.available(), reason="libcrdt_host.so
 
 def test_library_exports_every_header_symbol():
     txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "crdt_host.h")).read(), flags=re.S)
-    declared = set(re.findall(r"^\s*(?:int|void|uint64_t|uint32_t|crdt_keys\*)\s+(crdt_\w+)\s*\(", txt, flags=re.M))
+    declared = set(re.findall(r"^\s*(?:int|void|uint64_t|uint32_t|crdt_keys\*|const char\*)\s+(crdt_\w+)\s*\(", txt, flags=re.M))
     assert declared == set(hostlib.SIGNATURES), declared ^ set(hostlib.SIGNATURES)
     out = subprocess.run(["nm", "-D", "--defined-only", hostlib.LIB_PATH], capture_output=True, text=True).stdout
     assert declared <= set(re.findall(r" T (crdt_\w+)", out))
-    assert ctypes.CDLL(hostlib.LIB_PATH).crdt_host_abi_version() == 1
+    assert ctypes.CDLL(hostlib.LIB_PATH).crdt_host_abi_version() == 2
 
 
 def _native_records(dec, keys: KeyIndex):

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host-ingest throughput: CrdtJson.decode of an N-record document by the native
 decoder (libcrdt_host.so) vs the Python restatement, and (with --gpu) MapCrdt.mergeJson
-end to end on the GPU both ways.  Prints one JSON line."""
+end to end on the GPU both ways, then the export (MapCrdt.toJson of the merged map:
+device compaction + native encode vs the Python restatement).  Prints one JSON line."""
 import argparse
 import json
 import os
@@ -62,6 +63,19 @@ def main():
             out[f"mergeJson_{mode}_s"] = round(time.perf_counter() - t, 3)
             assert c.last_ingest == mode
             out[f"mergeJson_{mode}_rps"] = round(a.records / out[f"mergeJson_{mode}_s"])
+            # export of the merged map: raw input spans (native ingest) or Python values (python)
+            from crdt_amd.crdt import Crdt
+            t = time.perf_counter()
+            js = c.toJson()
+            out[f"toJson_native_{mode}vals_s"] = round(time.perf_counter() - t, 3)
+            assert c.last_export == "native"
+            if mode == "native":
+                t = time.perf_counter()
+                ref = Crdt.toJson(c)
+                out["toJson_python_s"] = round(time.perf_counter() - t, 3)
+                assert js == ref
+                out["toJson_native_rps"] = round((a.records + 1) / out["toJson_native_nativevals_s"])
+                out["toJson_python_rps"] = round((a.records + 1) / out["toJson_python_s"])
     print(json.dumps(out))
 
 
