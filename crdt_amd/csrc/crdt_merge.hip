@@ -97,7 +97,7 @@ struct Misc {
     uint32_t cand_count;   // candidate tiles appended by k_scan
     uint32_t stop;         // changesets to apply (set by k_resolve)
     uint32_t err;          // key range violation
-    uint32_t pad;
+    uint32_t vdone;        // k_verify<true> workgroups finished (the last one resolves)
     crdt_result result;    // filled by k_resolve
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
@@ -216,13 +216,21 @@ __device__ inline bool send_fails(int64_t r, int64_t wall) {
     return wsub(mn, wall) > kMaxDrift || cn > kMaxCounter;
 }
 
+// kTiles (small batches: <= kClockTilesMax tiles, R <= kClockRMax): M_j is reduced here from the
+// scan's tile maxima T (LDS max per changeset) instead of by a separate k_tmax launch.
+constexpr uint32_t kClockTilesMax = 1u << 16;
+constexpr uint32_t kClockRMax = 2048;
+
+template <bool kTiles>
 __global__ __launch_bounds__(1024) void k_clock(
-    const long long* __restrict__ M, uint32_t R, int64_t wall, int64_t c0,
+    const long long* __restrict__ M, const int64_t* __restrict__ T, const uint32_t* __restrict__ tstart,
+    uint32_t R, int64_t wall, int64_t c0,
     int64_t* __restrict__ Cprev, int64_t* __restrict__ Rj, int64_t* __restrict__ Cj,
     long long* __restrict__ event)
 {
     __shared__ int64_t s_wave[16];
     __shared__ uint32_t s_first;
+    __shared__ long long s_M[kTiles ? kClockRMax : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t W = (int64_t)((uint64_t)wall << kShift);
     int64_t carry = c0;                       // D_0 = C_0
@@ -231,12 +239,25 @@ __global__ __launch_bounds__(1024) void k_clock(
         s_first = UINT32_MAX;
         event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN;   // = k_event_init
     }
+    if (kTiles) {
+        for (uint32_t j = tid; j < R; j += 1024) s_M[j] = INT64_MIN;
+        __syncthreads();
+        const uint32_t nt = tstart[R];
+        for (uint32_t u = tid; u < nt; u += 1024) {
+            uint32_t lo = 0, hi = R;                 // changeset of tile u: largest j with tstart[j] <= u
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (tstart[mid] <= u) lo = mid; else hi = mid;
+            }
+            atomicMax(&s_M[lo], (long long)T[u]);
+        }
+    }
     __syncthreads();
     for (uint32_t base = 0; base < R; base += 1024) {
         const uint32_t j = base + tid;
         const bool valid = j < R;
         const int64_t jj = (int64_t)j + 1;
-        const int64_t mj = valid ? (int64_t)M[j] : INT64_MIN;
+        const int64_t mj = valid ? (int64_t)(kTiles ? s_M[j] : M[j]) : INT64_MIN;
         const bool has = mj != INT64_MIN;
         const int64_t b = has ? imax(mj + 1, W) : W;
         const int64_t key = valid ? b - jj : INT64_MIN;
@@ -277,22 +298,108 @@ __global__ __launch_bounds__(1024) void k_clock(
         atomicMin(event, (long long)(((int64_t)s_first << kLowBits) | kLowMask));
 }
 
+// Publish the recv-failure details of the global first event if this ctx holds
+// it: event[1] = canonical at the failure, event[2] = kind, event[3] = Hlc.millis.
+// (Every thread of the workgroup calls it.)
+__device__ void resolve_local_body(const Misc* __restrict__ misc, const long long* __restrict__ cand_key,
+                                   const int64_t* __restrict__ cand_P, const uint32_t* __restrict__ cand_kind,
+                                   const int64_t* __restrict__ cand_ms, long long* __restrict__ event)
+{
+    const long long ev = event[0];
+    __syncthreads();                           // every thread read event[0] before it is rewritten
+    if (threadIdx.x == 0) { event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
+    __syncthreads();
+    if (ev == kEvNone || (ev & kLowMask) == kLowMask) return;
+    const uint32_t n = misc->cand_count;
+    for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
+        if (cand_key[c] == ev) {
+            event[1] = cand_P[c];
+            event[2] = cand_kind[c];
+            event[3] = cand_ms[c];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_resolve_local(
+    const Misc* __restrict__ misc, const long long* __restrict__ cand_key,
+    const int64_t* __restrict__ cand_P, const uint32_t* __restrict__ cand_kind,
+    const int64_t* __restrict__ cand_ms, long long* __restrict__ event)
+{
+    resolve_local_body(misc, cand_key, cand_P, cand_kind, cand_ms, event);
+}
+
+// =============================================================================
+// K3d — k_resolve: stop point, status, final canonical (crdt.dart:80-93 order:
+// every recv of changeset j, then its store, then its send).  Thread 0 only.
+// =============================================================================
+__device__ void resolve_body(const long long* __restrict__ event, uint32_t R, int64_t wall,
+                             int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
+                             Misc* __restrict__ misc)
+{
+    crdt_result res = {};
+    res.exc_index = UINT64_MAX;
+    const int64_t ev = event[0];
+    uint32_t stop;
+    if (ev == kEvNone) {
+        stop = R;
+        res.status = CRDT_OK;
+        res.canonical_lt = R ? Cj[R - 1] : c0;
+    } else {
+        const uint32_t j = (uint32_t)(ev >> kLowBits);
+        const int64_t low = ev & kLowMask;
+        res.exc_changeset = j;
+        if (low == kLowMask) {                       // send() after storing changeset j
+            stop = j + 1;
+            const int64_t r = Rj[j];
+            const int64_t m = r >> kShift, c = r & kMaxCounter;
+            const int64_t mn = imax(m, wall);
+            res.canonical_lt = r;
+            if (wsub(mn, wall) > kMaxDrift) {
+                res.status = CRDT_CLOCK_DRIFT;
+                res.drift_ms = wsub(mn, wall);
+            } else {
+                res.status = CRDT_OVERFLOW;
+                res.counter = c + 1;
+            }
+        } else {                                     // recv() inside changeset j
+            stop = j;
+            res.exc_index = (uint64_t)low;
+            res.canonical_lt = event[1];
+            res.status = (int32_t)event[2];
+            if (res.status == CRDT_CLOCK_DRIFT) res.drift_ms = wsub(event[3], wall);
+        }
+    }
+    res.n_stored = stop;
+    misc->stop = stop;
+    misc->result = res;
+}
+
+__global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64_t wall,
+                          int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
+                          Misc* __restrict__ misc)
+{
+    if (threadIdx.x == 0) resolve_body(event, R, wall, c0, Rj, Cj, misc);
+}
+
 // =============================================================================
 // K3c — k_verify: for each candidate tile, the first record i (in iteration
 // order) with flag(i) && lt_i > max(C_{j-1}, lt of every earlier record of j),
 // i.e. the first Hlc.recv that throws (hlc.dart:85-94).  One wave per tile,
 // ordered 64-record rounds with a shuffle prefix max.  Rare path.
 // =============================================================================
+// kFuse (single-ctx crdt_merge): the last workgroup to finish also runs k_resolve_local and
+// k_resolve (Rj / Cj / c0 only read then), saving two launches per merge call.
+template <bool kFuse>
 __global__ __launch_bounds__(64) void k_verify(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t R, const int64_t* __restrict__ T,
     const int64_t* __restrict__ Cprev, int64_t wall, uint32_t local_rank,
-    const Misc* __restrict__ misc, const uint32_t* __restrict__ cand_tile,
+    Misc* __restrict__ misc, const uint32_t* __restrict__ cand_tile,
     long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
     uint32_t* __restrict__ cand_kind, int64_t* __restrict__ cand_ms,
     const long long* __restrict__ pbase, const unsigned long long* __restrict__ ibase,
-    long long* __restrict__ event)
+    long long* __restrict__ event, int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj)
 {
     // pbase / ibase (optional): this ctx holds only a PART of changeset j, preceded in
     // its iteration order by records of other ranks whose max lt is pbase[j] and whose
@@ -357,74 +464,18 @@ __global__ __launch_bounds__(64) void k_verify(
             }
         }
     }
-}
-
-// Publish the recv-failure details of the global first event if this ctx holds
-// it: event[1] = canonical at the failure, event[2] = kind, event[3] = Hlc.millis.
-__global__ __launch_bounds__(256) void k_resolve_local(
-    const Misc* __restrict__ misc, const long long* __restrict__ cand_key,
-    const int64_t* __restrict__ cand_P, const uint32_t* __restrict__ cand_kind,
-    const int64_t* __restrict__ cand_ms, long long* __restrict__ event)
-{
-    const long long ev = event[0];
-    if (threadIdx.x == 0) { event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
-    __syncthreads();
-    if (ev == kEvNone || (ev & kLowMask) == kLowMask) return;
-    const uint32_t n = misc->cand_count;
-    for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
-        if (cand_key[c] == ev) {
-            event[1] = cand_P[c];
-            event[2] = cand_kind[c];
-            event[3] = cand_ms[c];
-        }
+    if (kFuse) {
+        __shared__ uint32_t s_last;
+        __threadfence();                       // this workgroup's candidate words and event min
+        if (lane == 0) s_last = atomicAdd(&misc->vdone, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();                       // acquire: every other workgroup's writes
+        resolve_local_body(misc, cand_key, cand_P, cand_kind, cand_ms, event);
+        __syncthreads();
+        __threadfence_block();
+        if (lane == 0) resolve_body(event, R, wall, c0, Rj, Cj, misc);
     }
-}
-
-// =============================================================================
-// K3d — k_resolve: stop point, status, final canonical (crdt.dart:80-93 order:
-// every recv of changeset j, then its store, then its send).
-// =============================================================================
-__global__ void k_resolve(const long long* __restrict__ event, uint32_t R, int64_t wall,
-                          int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
-                          Misc* __restrict__ misc)
-{
-    if (threadIdx.x != 0) return;
-    crdt_result res = {};
-    res.exc_index = UINT64_MAX;
-    const int64_t ev = event[0];
-    uint32_t stop;
-    if (ev == kEvNone) {
-        stop = R;
-        res.status = CRDT_OK;
-        res.canonical_lt = R ? Cj[R - 1] : c0;
-    } else {
-        const uint32_t j = (uint32_t)(ev >> kLowBits);
-        const int64_t low = ev & kLowMask;
-        res.exc_changeset = j;
-        if (low == kLowMask) {                       // send() after storing changeset j
-            stop = j + 1;
-            const int64_t r = Rj[j];
-            const int64_t m = r >> kShift, c = r & kMaxCounter;
-            const int64_t mn = imax(m, wall);
-            res.canonical_lt = r;
-            if (wsub(mn, wall) > kMaxDrift) {
-                res.status = CRDT_CLOCK_DRIFT;
-                res.drift_ms = wsub(mn, wall);
-            } else {
-                res.status = CRDT_OVERFLOW;
-                res.counter = c + 1;
-            }
-        } else {                                     // recv() inside changeset j
-            stop = j;
-            res.exc_index = (uint64_t)low;
-            res.canonical_lt = event[1];
-            res.status = (int32_t)event[2];
-            if (res.status == CRDT_CLOCK_DRIFT) res.drift_ms = wsub(event[3], wall);
-        }
-    }
-    res.n_stored = stop;
-    misc->stop = stop;
-    misc->result = res;
 }
 
 // =============================================================================
@@ -820,6 +871,8 @@ struct crdt_ctx {
     DBuf<int64_t> p_kslt;
     HBuf<uint64_t> h_pplan;
     bool last_sorted = false;       // the last crdt_merge ran the sorted path
+    bool fused = false;             // this plan: tile max in k_clock<true>, resolve in k_verify<true>
+    bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
 };
 
@@ -942,7 +995,11 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 }
 
 // ---- phases ---------------------------------------------------------------
-int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima) {
+// allow_fuse (single-ctx crdt_merge): for small batches the tile-max reduction moves into
+// k_clock<true> and the resolve kernels into the last k_verify<true> workgroup (c->fused).
+int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false) {
+    c->fused = false;
+    c->resolved = false;
     int st = validate_batch(home);
     if (st) return st;
     const uint32_t R = home->n_changesets;
@@ -963,6 +1020,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
                                                                                      INT64_MIN);
     c->plan_R = R;
     c->plan_tiles = tiles;
+    c->fused = allow_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
         const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
@@ -973,7 +1031,8 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
                 cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                 c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
         }
-        k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);
+        if (!c->fused)
+            k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);
         HIPCHK(hipGetLastError());
     }
     return CRDT_OK;
@@ -998,13 +1057,24 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
         d_ibase = c->d_ibase.p;
     }
     if (!R) k_event_init<<<1, 64, 0, c->stream>>>(d_event);   // else k_clock initialises the words
-    if (R) k_clock<<<1, 1024, 0, c->stream>>>(d_maxima, R, wall, c->canonical, c->d_Cprev.p, c->d_Rj.p,
-                                              c->d_Cj.p, d_event);
-    if (c->plan_tiles)
-        k_verify<<<kVerifyBlocks, 64, 0, c->stream>>>(
+    if (c->fused) {                                           // (plan_tiles > 0, R <= kClockRMax)
+        k_clock<true><<<1, 1024, 0, c->stream>>>(nullptr, c->d_T.p, c->d_tstart, R, wall, c->canonical,
+                                                 c->d_Cprev.p, c->d_Rj.p, c->d_Cj.p, d_event);
+        k_verify<true><<<kVerifyBlocks, 64, 0, c->stream>>>(
             cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, R, c->d_T.p, c->d_Cprev.p, wall,
             c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
-            c->d_candms.p, d_pbase, d_ibase, d_event);
+            c->d_candms.p, d_pbase, d_ibase, d_event, c->canonical, c->d_Rj.p, c->d_Cj.p);
+        c->resolved = true;                                   // misc->stop / result are set
+        HIPCHK(hipGetLastError());
+        return CRDT_OK;
+    }
+    if (R) k_clock<false><<<1, 1024, 0, c->stream>>>(d_maxima, nullptr, nullptr, R, wall, c->canonical,
+                                                     c->d_Cprev.p, c->d_Rj.p, c->d_Cj.p, d_event);
+    if (c->plan_tiles)
+        k_verify<false><<<kVerifyBlocks, 64, 0, c->stream>>>(
+            cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, R, c->d_T.p, c->d_Cprev.p, wall,
+            c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
+            c->d_candms.p, d_pbase, d_ibase, d_event, 0, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     return CRDT_OK;
 }
@@ -1031,7 +1101,9 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
         }
         if (n) HIPCHK(hipMemsetAsync(dflags, 0, n, c->stream));
     }
-    k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    if (!c->resolved)
+        k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    c->resolved = false;
     ev_record(c, ev_base);
     c->windows.clear();
     uint32_t nl = 0;
@@ -1098,7 +1170,9 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
 int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wall, const long long* d_event,
                  crdt_result* out, size_t ev_base) {
     const uint32_t R = c->plan_R;
-    k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    if (!c->resolved)
+        k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+    c->resolved = false;
     ev_record(c, ev_base);
     c->windows.clear();
     c->apply_total = 1;
@@ -1633,10 +1707,10 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     HIPALLOC(c->d_M.ensure(R));
     if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
     ev_record(c, 0);
-    if ((st = phase_scan(c, &dev, wall, c->d_M.p))) return st;
+    if ((st = phase_scan(c, &dev, wall, c->d_M.p, true))) return st;
     ev_record(c, 1);
     if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
-    if ((st = phase_resolve(c, c->d_event.p))) return st;
+    if (!c->resolved && (st = phase_resolve(c, c->d_event.p))) return st;
     ev_record(c, 2);
     st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, 3, true);
     if (c->timing) {
