@@ -98,6 +98,8 @@ struct Misc {
     uint32_t stop;         // changesets to apply (set by k_resolve)
     uint32_t err;          // key range violation
     uint32_t vdone;        // k_verify<true> workgroups finished (the last one resolves)
+    uint32_t tiles_hot;    // scan tiles holding a record above C_0, every kHotSample-th (next scan's form)
+    uint32_t pad;
     crdt_result result;    // filled by k_resolve
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
@@ -131,6 +133,12 @@ __device__ inline int64_t wave_scan_max_incl(int64_t v, int lane) {
 // hlc.dart:88-90; millis - wall > 60000: ClockDrift, hlc.dart:92-94) AND its lt
 // exceeds the canonical; canonicals never decrease, so lt <= C_0 can never raise.
 // =============================================================================
+constexpr uint32_t kHotSample = 16;              // tiles_hot counts every 16th tile (one address)
+
+// kEager: rank / millis are loaded with lt instead of after it (one memory round trip per
+// tile instead of two) — chosen when the previous call found most tiles above C_0 (streaming
+// deltas); otherwise only waves holding such a record load them (the fan-in: ~none do).
+template <bool kEager>
 __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
@@ -149,24 +157,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         int64_t m = INT64_MIN;
         int f = 0;
         int64_t v[kScanItems];
+        uint32_t rk[kEager ? kScanItems : 1];
+        int64_t mv[kEager ? kScanItems : 1];
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
             v[q] = i < end ? lt[i] : INT64_MIN;
+            if (kEager) {
+                rk[q] = i < end ? rank[i] : 0u;
+                mv[q] = (millis && i < end) ? millis[i] : 0;
+            }
             m = imax(m, v[q]);
         }
-        // rank / millis matter only for records above C0 (the only ones recv() can raise on):
-        // a wave with none issues no load for them (the fan-in: ~all of them)
+        // rank / millis matter only for records above C0 (the only ones recv() can raise on)
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             if (v[q] > c0) {
                 const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-                const int64_t ms = millis ? millis[i] : (v[q] >> kShift);
-                f |= (rank[i] == local_rank) | (wsub(ms, wall) > kMaxDrift);
+                const int64_t ms = millis ? (kEager ? mv[kEager ? q : 0] : millis[i]) : (v[q] >> kShift);
+                const uint32_t r = kEager ? rk[kEager ? q : 0] : rank[i];
+                f |= (r == local_rank) | (wsub(ms, wall) > kMaxDrift);
             }
         }
         m = wave_max(m);
-        const int fw = __any(f);
+        const int fw = __any(f) | (m > c0 ? 2 : 0);
         if (lane == 0) { s_max[w] = m; s_flag[w] = fw; }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -174,10 +188,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             int tf = s_flag[0];
             for (int k = 1; k < kScanThreads / 64; ++k) { tm = imax(tm, s_max[k]); tf |= s_flag[k]; }
             T[t0 + t] = tm;
-            if (tf) {
+            if (tf & 1) {
                 const uint32_t c = atomicAdd(&misc->cand_count, 1u);
                 cand_tile[c] = t0 + t;
             }
+            if ((tf & 2) && ((t0 + t) & (kHotSample - 1)) == 0) atomicAdd(&misc->tiles_hot, 1u);   // sampled
         }
         __syncthreads();
     }
@@ -872,6 +887,7 @@ struct crdt_ctx {
     HBuf<uint64_t> h_pplan;
     bool last_sorted = false;       // the last crdt_merge ran the sorted path
     bool fused = false;             // this plan: tile max in k_clock<true>, resolve in k_verify<true>
+    bool scan_eager = false;        // next k_scan loads rank / millis with lt (last call: mostly hot tiles)
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
 };
@@ -1027,9 +1043,14 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            k_scan<<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
-                cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            if (c->scan_eager)
+                k_scan<true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            else
+                k_scan<false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
         }
         if (!c->fused)
             k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);
@@ -1153,6 +1174,7 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
         HIPCHK(hipMemcpyAsync(win_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     crdt_result res = c->h_misc->result;
+    c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
     uint64_t np = 0, nw = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
     res.n_present = np;
@@ -1289,6 +1311,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
     }
 #endif
     crdt_result res = c->h_misc->result;
+    c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
     uint64_t np = 0, nw_ = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw_ += c->h_misc->won[s]; }
     res.n_present = np;
