@@ -233,7 +233,7 @@ __device__ inline bool send_fails(int64_t r, int64_t wall) {
 
 // kTiles (small batches: <= kClockTilesMax tiles, R <= kClockRMax): M_j is reduced here from the
 // scan's tile maxima T (LDS max per changeset) instead of by a separate k_tmax launch.
-constexpr uint32_t kClockTilesMax = 1u << 16;
+constexpr uint32_t kClockTilesMax = 8192;         // <= 8 tiles per thread (cfg3's 24K tiles: k_tmax is faster)
 constexpr uint32_t kClockRMax = 2048;
 
 template <bool kTiles>
@@ -246,6 +246,7 @@ __global__ __launch_bounds__(1024) void k_clock(
     __shared__ int64_t s_wave[16];
     __shared__ uint32_t s_first;
     __shared__ long long s_M[kTiles ? kClockRMax : 1];
+    __shared__ uint32_t s_ts[kTiles ? kClockRMax + 1 : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t W = (int64_t)((uint64_t)wall << kShift);
     int64_t carry = c0;                       // D_0 = C_0
@@ -255,16 +256,20 @@ __global__ __launch_bounds__(1024) void k_clock(
         event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN;   // = k_event_init
     }
     if (kTiles) {
-        for (uint32_t j = tid; j < R; j += 1024) s_M[j] = INT64_MIN;
+        for (uint32_t j = tid; j <= R; j += 1024) {
+            s_ts[j] = tstart[j];
+            if (j < R) s_M[j] = INT64_MIN;
+        }
         __syncthreads();
-        const uint32_t nt = tstart[R];
+        const uint32_t nt = s_ts[R];
         for (uint32_t u = tid; u < nt; u += 1024) {
+            const int64_t tu = T[u];
             uint32_t lo = 0, hi = R;                 // changeset of tile u: largest j with tstart[j] <= u
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (tstart[mid] <= u) lo = mid; else hi = mid;
+                if (s_ts[mid] <= u) lo = mid; else hi = mid;
             }
-            atomicMax(&s_M[lo], (long long)T[u]);
+            atomicMax(&s_M[lo], (long long)tu);
         }
     }
     __syncthreads();
