@@ -1308,11 +1308,31 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         unsigned long long pr[8];
         hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprof), sizeof(pr));
         fprintf(stderr, "[rprof] items %llu chunks %llu | per item: init %.2f us final %.2f us | per chunk: "
-                "A %.2f us B %.2f us\n", pr[4], pr[5], pr[0] / 100.0 / (pr[4] ? pr[4] : 1),
-                pr[3] / 100.0 / (pr[4] ? pr[4] : 1), pr[1] / 100.0 / (pr[5] ? pr[5] : 1),
-                pr[2] / 100.0 / (pr[5] ? pr[5] : 1));
+                "A %.2f us B %.2f us | max chunk B %.2f us, max item %.2f us\n", pr[4], pr[5],
+                pr[0] / 100.0 / (pr[4] ? pr[4] : 1), pr[3] / 100.0 / (pr[4] ? pr[4] : 1),
+                pr[1] / 100.0 / (pr[5] ? pr[5] : 1), pr[2] / 100.0 / (pr[5] ? pr[5] : 1), pr[6] / 100.0,
+                pr[7] / 100.0);
         memset(pr, 0, sizeof(pr));
         hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), pr, sizeof(pr));
+        static std::vector<unsigned long long> it(1 << 18);
+        hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_item_dur), it.size() * 8);
+        uint64_t hist[8] = {0}, hsum[8] = {0};           // by duration: <25, <50, <100, <200, <400, <800, <1600, more us
+        unsigned long long top = 0;
+        size_t top_i = 0;
+        for (size_t i = 0; i < it.size(); ++i) {
+            const double us = (it[i] >> 24) / 100.0;
+            if (!it[i]) continue;
+            int b = us < 25 ? 0 : us < 50 ? 1 : us < 100 ? 2 : us < 200 ? 3 : us < 400 ? 4 : us < 800 ? 5 : us < 1600 ? 6 : 7;
+            hist[b]++;
+            hsum[b] += (it[i] >> 8) & 0xFFFF;
+            if (it[i] > top) { top = it[i]; top_i = i; }
+        }
+        fprintf(stderr, "[rprof] items by duration <25/50/100/200/400/800/1600/more us: ");
+        for (int b = 0; b < 8; ++b) fprintf(stderr, "%llu(%.1f ch) ", (unsigned long long)hist[b], hist[b] ? (double)hsum[b] / hist[b] : 0.0);
+        fprintf(stderr, "| slowest item %zu: %.1f us, %llu chunks, flags %llu\n", top_i, (top >> 24) / 100.0,
+                (top >> 8) & 0xFFFF, top & 3);
+        std::fill(it.begin(), it.end(), 0ull);
+        hipMemcpyToSymbol(HIP_SYMBOL(g_item_dur), it.data(), it.size() * 8);
     }
 #endif
     crdt_result res = c->h_misc->result;
