@@ -20,7 +20,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
+#include <algorithm>
+#include <functional>
 #include <new>
+#include <thread>
 #include <string>
 #include <string_view>
 #include <unordered_set>
@@ -127,6 +132,34 @@ struct crdt_keys {
         arena.reserve(arena.size() + more_bytes);
         off.reserve(want + 1);
         hash.reserve(want);
+    }
+
+    void prefetch(uint64_t h) const {
+        if (!slot.empty()) __builtin_prefetch(slot.data() + (h & mask));
+    }
+
+    // One probe sequence: true with *id when present, else the key is added (next id), false.
+    bool find_or_add(const char* p, uint64_t n, uint64_t h, uint32_t* id) {
+        if ((hash.size() + 1) * 2 > slot.size()) rebuild(hash.size() + 1 > 8 ? (hash.size() + 1) * 2 : 16);
+        const uint64_t hi = h & 0xFFFFFFFF00000000ull;
+        uint64_t s = h & mask;
+        for (;; s = (s + 1) & mask) {
+            const uint64_t v = slot[s];
+            if (!v) break;
+            if ((v & 0xFFFFFFFF00000000ull) != hi) continue;
+            const uint32_t i = (uint32_t)v - 1;
+            if (off[i + 1] - off[i] == n && memcmp(arena.data() + off[i], p, n) == 0) {
+                *id = i;
+                return true;
+            }
+        }
+        const uint32_t nid = (uint32_t)hash.size();
+        arena.insert(arena.end(), p, p + n);
+        off.push_back(arena.size());
+        hash.push_back(h);
+        slot[s] = hi | (uint64_t)(nid + 1);
+        *id = nid;
+        return false;
     }
 
     uint32_t add(const char* p, uint64_t n, uint64_t h) {
@@ -413,6 +446,9 @@ struct IdMap {
         mask = cap - 1;
         used = 0;
     }
+    void prefetch(uint32_t id) const {
+        __builtin_prefetch(s.data() + ((((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 20) & mask));
+    }
     // returns the record index of id, or inserts rec and returns UINT32_MAX
     uint32_t get_or_put(uint32_t id, uint32_t rec) {
         if ((used + 1) * 2 > s.size()) {
@@ -443,127 +479,350 @@ struct IdMap {
     }
 };
 
-int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
-    Parser p{js, len, 0, std::string()};
-    const uint64_t n0 = keys->size();
+// One record `"<key>": {"hlc": <string>, "value": <any>, ...}` at p (after '{' or ','):
+// the key (decoded UTF-8 into *key), Hlc.parse of hlc -> lt + node id span, value span.
+struct RecordText {
+    int64_t lt;
+    const char* node;            // into the input (Hlc strings never need unescaping here: a
+    uint64_t node_len;           // node id with an escape is copied into node_buf)
+    uint64_t voff;
+    uint32_t vlen;
+};
+
+void parse_record(Parser& p, const char* js, std::string& key, std::string& node_buf, RecordText& r) {
+    const char* kp;
+    uint64_t kl;
+    p.string(&kp, &kl);
+    key.assign(kp, kl);                               // p.tmp is reused below
+    p.ws();
+    p.expect(':');
+    p.ws();
+    // the record object: {"hlc": <string>, "value": <any>, ...}; a repeated field: last wins
+    if (p.peek() != '{') throw Fallback();
+    ++p.i;
+    bool have_hlc = false;
+    r.voff = 0;
+    r.vlen = 0;
+    p.ws();
+    if (p.peek() == '}') {
+        ++p.i;
+    } else {
+        while (true) {
+            p.ws();
+            const char* fp;
+            uint64_t fl;
+            p.string(&fp, &fl);
+            const bool is_hlc = fl == 3 && memcmp(fp, "hlc", 3) == 0;
+            const bool is_val = fl == 5 && memcmp(fp, "value", 5) == 0;
+            p.ws();
+            p.expect(':');
+            p.ws();
+            if (is_hlc) {
+                if (p.peek() != '"') throw Fallback();
+                const char* hp;
+                uint64_t hl;
+                p.string(&hp, &hl);
+                uint64_t npos;
+                if (!parse_hlc(hp, hl, &r.lt, &npos)) throw Fallback();
+                node_buf.assign(hp + npos, hl - npos);
+                have_hlc = true;
+            } else if (is_val) {
+                const uint64_t b = p.i;
+                p.skip_value(1);
+                const bool is_null = p.i - b == 4 && memcmp(js + b, "null", 4) == 0;
+                if (p.i - b >= (1ull << 32)) throw Fallback();
+                r.voff = is_null ? 0 : b;
+                r.vlen = is_null ? 0 : (uint32_t)(p.i - b);
+            } else {
+                p.skip_value(1);
+            }
+            p.ws();
+            if (p.peek() == ',') { ++p.i; continue; }
+            p.expect('}');
+            break;
+        }
+    }
+    if (!have_hlc) throw Fallback();                  // Hlc.parse(null) throws
+    r.node = node_buf.data();
+    r.node_len = node_buf.size();
+}
+
+// Per-document builder of the output columns: node ids in first-seen order, key ids from the
+// table (new keys appended in document order), a repeated key keeps its first position and
+// its last record (jsonDecode into a LinkedHashMap).
+struct Builder {
+    crdt_keys* keys;
+    crdt_decoded* d;
+    uint64_t n0;                                      // table size before the document
     std::unordered_map<std::string, uint32_t> node_ix;
-    IdMap seen;
-    const uint64_t est = len / 48 + 16;                  // a record is >= ~48 bytes of JSON
-    seen.init(est);
-    keys->reserve(est, len / 4);
-    d->key.reserve(est); d->lt.reserve(est); d->node.reserve(est); d->voff.reserve(est); d->vlen.reserve(est);
-    const char* last_node = nullptr;                    // records of one changeset mostly share a node
+    IdMap seen;                                       // keys that existed before: id -> first record
+    std::vector<uint32_t> first_new;                  // keys added by the document: first record
+    const char* last_node = nullptr;                  // records of one changeset mostly share a node
     uint64_t last_len = 0;
     uint32_t last_nid = 0;
-    std::string kbuf;
-    try {
-        p.ws();
-        p.expect('{');
-        p.ws();
-        if (p.peek() == '}') {
-            ++p.i;
+
+    Builder(crdt_keys* k, crdt_decoded* dd) : keys(k), d(dd), n0(k->size()) { seen.init(64); }
+
+    uint32_t node_id(const char* np, uint64_t nl) {
+        if (last_node && nl == last_len && memcmp(np, last_node, nl) == 0) return last_nid;
+        const std::string node(np, nl);
+        auto it = node_ix.find(node);
+        uint32_t nid;
+        if (it == node_ix.end()) {
+            nid = (uint32_t)d->nodes.size();
+            node_ix.emplace(node, nid);
+            d->nodes.push_back(node);
         } else {
-            while (true) {
-                p.ws();
-                const char* kp;
-                uint64_t kl;
-                p.string(&kp, &kl);
-                kbuf.assign(kp, kl);                       // p.tmp is reused below
-                p.ws();
-                p.expect(':');
-                p.ws();
-                // the record object: {"hlc": <string>, "value": <any>, ...}; last duplicate wins
-                if (p.peek() != '{') throw Fallback();
-                ++p.i;
-                bool have_hlc = false;
-                int64_t lt = 0;
-                std::string node;
-                uint64_t voff = 0;
-                uint32_t vlen = 0;
-                p.ws();
-                if (p.peek() == '}') {
-                    ++p.i;
-                } else {
-                    while (true) {
-                        p.ws();
-                        const char* fp;
-                        uint64_t fl;
-                        p.string(&fp, &fl);
-                        const bool is_hlc = fl == 3 && memcmp(fp, "hlc", 3) == 0;
-                        const bool is_val = fl == 5 && memcmp(fp, "value", 5) == 0;
-                        p.ws();
-                        p.expect(':');
-                        p.ws();
-                        if (is_hlc) {
-                            if (p.peek() != '"') throw Fallback();
-                            const char* hp;
-                            uint64_t hl;
-                            p.string(&hp, &hl);
-                            uint64_t npos;
-                            if (!parse_hlc(hp, hl, &lt, &npos)) throw Fallback();
-                            node.assign(hp + npos, hl - npos);
-                            have_hlc = true;
-                        } else if (is_val) {
-                            const uint64_t b = p.i;
-                            p.skip_value(1);
-                            const bool is_null = p.i - b == 4 && memcmp(js + b, "null", 4) == 0;
-                            if (p.i - b >= (1ull << 32)) throw Fallback();
-                            voff = is_null ? 0 : b;
-                            vlen = is_null ? 0 : (uint32_t)(p.i - b);
-                        } else {
-                            p.skip_value(1);
-                        }
-                        p.ws();
-                        if (p.peek() == ',') { ++p.i; continue; }
-                        p.expect('}');
-                        break;
-                    }
-                }
-                if (!have_hlc) throw Fallback();           // Hlc.parse(null) throws
-                uint32_t nid;
-                if (last_node && node.size() == last_len && memcmp(node.data(), last_node, last_len) == 0) {
-                    nid = last_nid;
-                } else {
-                    auto it = node_ix.find(node);
-                    if (it == node_ix.end()) {
-                        nid = (uint32_t)d->nodes.size();
-                        node_ix.emplace(node, nid);
-                        d->nodes.push_back(node);
-                    } else {
-                        nid = it->second;
-                    }
-                    last_node = d->nodes[nid].data();
-                    last_len = d->nodes[nid].size();
-                    last_nid = nid;
-                }
-                const uint64_t h = hash_bytes(kbuf.data(), kbuf.size());
-                uint32_t id;
-                if (!keys->find(kbuf.data(), kbuf.size(), h, &id)) {
-                    if (keys->size() >= 0xFFFFFFF0ull) throw Fallback();
-                    id = keys->add(kbuf.data(), kbuf.size(), h);
-                }
-                const uint32_t rec = (uint32_t)d->key.size();
-                const uint32_t prev = seen.get_or_put(id, rec);
-                if (prev != UINT32_MAX) {                  // repeated key: first position, last record
-                    d->lt[prev] = lt;
-                    d->node[prev] = nid;
-                    d->voff[prev] = voff;
-                    d->vlen[prev] = vlen;
-                } else {
-                    d->key.push_back(id);
-                    d->lt.push_back(lt);
-                    d->node.push_back(nid);
-                    d->voff.push_back(voff);
-                    d->vlen.push_back(vlen);
-                }
-                p.ws();
-                if (p.peek() == ',') { ++p.i; continue; }
-                p.expect('}');
-                break;
-            }
+            nid = it->second;
         }
+        last_node = d->nodes[nid].data();
+        last_len = d->nodes[nid].size();
+        last_nid = nid;
+        return nid;
+    }
+
+    // id: the key's id when already known to exist (UINT32_MAX: look it up / add it now)
+    void add(const char* kp, uint64_t kl, uint64_t h, uint32_t id, int64_t lt, uint32_t nid, uint64_t voff,
+             uint32_t vlen) {
+        const uint32_t rec = (uint32_t)d->key.size();
+        uint32_t prev = UINT32_MAX;
+        bool fresh = false;
+        if (id == UINT32_MAX) {
+            if (keys->size() >= 0xFFFFFFF0ull) throw Fallback();
+            fresh = !keys->find_or_add(kp, kl, h, &id);
+        }
+        if (fresh) {
+            first_new.push_back(rec);                   // id == n0 + first_new.size() - 1
+        } else if (id >= n0) {
+            prev = first_new[id - n0];                  // repeated in this document
+        } else {
+            prev = seen.get_or_put(id, rec);
+        }
+        if (prev != UINT32_MAX) {                     // repeated key: first position, last record
+            d->lt[prev] = lt;
+            d->node[prev] = nid;
+            d->voff[prev] = voff;
+            d->vlen[prev] = vlen;
+        } else {
+            d->key.push_back(id);
+            d->lt.push_back(lt);
+            d->node.push_back(nid);
+            d->voff.push_back(voff);
+            d->vlen.push_back(vlen);
+        }
+    }
+};
+
+void begin_object(Parser& p) {
+    p.ws();
+    p.expect('{');
+    p.ws();
+}
+
+// After a record: true when another follows (p at its key), false at the closing '}'.
+bool next_record(Parser& p) {
+    p.ws();
+    if (p.peek() == ',') {
+        ++p.i;
         p.ws();
-        if (p.i != len) throw JsonError();
+        return true;
+    }
+    p.expect('}');
+    return false;
+}
+
+int decode_sequential(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
+    Parser p{js, len, 0, std::string()};
+    Builder bld(keys, d);
+    const uint64_t est = len / 48 + 16;               // a record is >= ~48 bytes of JSON
+    keys->reserve(est, len / 4);
+    d->key.reserve(est); d->lt.reserve(est); d->node.reserve(est); d->voff.reserve(est); d->vlen.reserve(est);
+    std::string key, node;
+    RecordText r;
+    begin_object(p);
+    if (p.peek() == '}') {
+        ++p.i;
+    } else {
+        do {
+            parse_record(p, js, key, node, r);
+            bld.add(key.data(), key.size(), hash_bytes(key.data(), key.size()), UINT32_MAX, r.lt,
+                    bld.node_id(r.node, r.node_len), r.voff, r.vlen);
+        } while (next_record(p));
+    }
+    p.ws();
+    if (p.i != len) throw JsonError();
+    return CRDT_HOST_OK;
+}
+
+// ---- parallel decode of a large document (CRDT_HOST_THREADS, default min(16, cores)).
+// Phase 1, one thread per byte range: the range's first record starts at the first `},"`
+// after its nominal start (speculative: the previous range verifies that its own parse ends
+// exactly there, else the rest is decoded sequentially); records are parsed into local
+// columns and their keys looked up (read-only) in the key table.  Phase 2, in order: node and
+// key ids are assigned and repeated keys folded exactly as the sequential decoder does.
+struct Chunk {
+    uint64_t beg = 0, lim = 0, stop = 0;   // parse from beg; records starting before lim; stop = where it ended
+    bool closed = false;                   // ended at the document's closing '}'
+    int status = CRDT_HOST_OK;
+    std::string karena;                    // decoded key bytes
+    std::vector<uint64_t> koff, khash;
+    std::vector<uint32_t> klen, kid, nid, vlen;
+    std::vector<int64_t> lt;
+    std::vector<uint64_t> voff;
+    std::vector<std::string> nodes;        // local node ids, first-seen order
+};
+
+void parse_chunk(const char* js, uint64_t len, const crdt_keys* keys, Chunk& c) {
+    Parser p{js, len, c.beg, std::string()};
+    std::string key, node;
+    std::unordered_map<std::string, uint32_t> nix;
+    RecordText r;
+    try {
+        do {
+            if (p.i >= c.lim) break;
+            parse_record(p, js, key, node, r);
+            const uint64_t h = hash_bytes(key.data(), key.size());
+            uint32_t id;
+            if (!keys->find(key.data(), key.size(), h, &id)) id = UINT32_MAX;
+            c.koff.push_back(c.karena.size());
+            c.karena.append(key);
+            c.klen.push_back((uint32_t)key.size());
+            c.khash.push_back(h);
+            c.kid.push_back(id);
+            c.lt.push_back(r.lt);
+            auto it = nix.find(node);
+            uint32_t ln;
+            if (it == nix.end()) {
+                ln = (uint32_t)c.nodes.size();
+                nix.emplace(node, ln);
+                c.nodes.push_back(node);
+            } else {
+                ln = it->second;
+            }
+            c.nid.push_back(ln);
+            c.voff.push_back(r.voff);
+            c.vlen.push_back(r.vlen);
+            if (!next_record(p)) { c.closed = true; break; }
+        } while (true);
+        c.stop = p.i;
+    } catch (const Fallback&) {
+        c.status = CRDT_HOST_FALLBACK;
+    } catch (const JsonError&) {
+        c.status = CRDT_HOST_E_JSON;
+    } catch (const std::bad_alloc&) {
+        c.status = CRDT_HOST_E_NOMEM;
+    }
+}
+
+int host_threads() {
+    if (const char* e = getenv("CRDT_HOST_THREADS")) {
+        const int v = atoi(e);
+        if (v >= 1) return v < 64 ? v : 64;
+    }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return hc == 0 ? 1 : (hc < 16 ? (int)hc : 16);
+}
+
+uint64_t parallel_min_bytes() {                       // CRDT_HOST_PAR_MIN: tests split small documents
+    if (const char* e = getenv("CRDT_HOST_PAR_MIN")) return strtoull(e, nullptr, 10);
+    return 4ull << 20;
+}
+
+int decode_parallel(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d, int nthreads) {
+    Parser p0{js, len, 0, std::string()};
+    begin_object(p0);
+    if (p0.peek() == '}') return decode_sequential(js, len, keys, d);
+    const uint64_t first = p0.i;
+    // chunk starts: chunk 0 at the first key; chunk k at the first `},"` after k * len / n
+    std::vector<uint64_t> starts{first};
+    for (int k = 1; k < nthreads; ++k) {
+        uint64_t g = std::max<uint64_t>((uint64_t)k * (len / nthreads), starts.back() + 1);
+        const char* f = nullptr;
+        while (g + 3 < len) {
+            f = static_cast<const char*>(memchr(js + g, '}', len - g));
+            if (!f) break;
+            const uint64_t q = f - js;
+            uint64_t r = q + 1;
+            while (r < len && (js[r] == ' ' || js[r] == '\t' || js[r] == '\n' || js[r] == '\r')) ++r;
+            if (r < len && js[r] == ',') {
+                ++r;
+                while (r < len && (js[r] == ' ' || js[r] == '\t' || js[r] == '\n' || js[r] == '\r')) ++r;
+                if (r < len && js[r] == '"') { g = r; break; }
+            }
+            g = q + 1;
+            f = nullptr;
+        }
+        if (!f) break;
+        starts.push_back(g);
+    }
+    const int n = (int)starts.size();
+    std::vector<Chunk> ch(n);
+    for (int k = 0; k < n; ++k) {
+        ch[k].beg = starts[k];
+        ch[k].lim = k + 1 < n ? starts[k + 1] : UINT64_MAX;
+    }
+    {
+        std::vector<std::thread> pool;
+        for (int k = 1; k < n; ++k) pool.emplace_back(parse_chunk, js, len, keys, std::ref(ch[k]));
+        parse_chunk(js, len, keys, ch[0]);
+        for (auto& t : pool) t.join();
+    }
+    // phase 2: chunks in order while each one's parse was valid and ended where the next began
+    Builder bld(keys, d);
+    uint64_t total = 0, kbytes = 0;
+    for (const auto& c : ch) { total += c.kid.size(); kbytes += c.karena.size(); }
+    keys->reserve(total, kbytes);
+    d->key.reserve(total); d->lt.reserve(total); d->node.reserve(total); d->voff.reserve(total); d->vlen.reserve(total);
+    uint64_t resume = 0;                                  // != 0: decode sequentially from here
+    bool closed = false;
+    std::vector<uint32_t> nmap;
+    for (int k = 0; k < n; ++k) {
+        const Chunk& c = ch[k];
+        if (c.status == CRDT_HOST_E_NOMEM) throw std::bad_alloc();
+        if (c.status == CRDT_HOST_FALLBACK) throw Fallback();   // valid start: this record is the first
+        if (c.status == CRDT_HOST_E_JSON) throw JsonError();    // failing one in document order
+        nmap.resize(c.nodes.size());
+        for (size_t m = 0; m < c.nodes.size(); ++m) nmap[m] = bld.node_id(c.nodes[m].data(), c.nodes[m].size());
+        const size_t nr = c.kid.size();
+        for (size_t m = 0; m < nr; ++m) {
+            if (m + 16 < nr) {                        // the table / first-record probes are cache misses
+                if (c.kid[m + 16] == UINT32_MAX) keys->prefetch(c.khash[m + 16]);
+                else bld.seen.prefetch(c.kid[m + 16]);
+            }
+            bld.add(c.karena.data() + c.koff[m], c.klen[m], c.khash[m], c.kid[m], c.lt[m], nmap[c.nid[m]], c.voff[m],
+                    c.vlen[m]);
+        }
+        if (c.closed) { closed = true; break; }
+        if (k + 1 < n && c.stop != starts[k + 1]) { resume = c.stop; break; }   // speculation failed
+        if (k + 1 == n) resume = c.stop;                  // (cannot happen: the last chunk has no limit)
+    }
+    if (!closed) {
+        // the rest, sequentially, from a verified record start
+        Parser p{js, len, resume, std::string()};
+        std::string key, node;
+        RecordText r;
+        do {
+            parse_record(p, js, key, node, r);
+            bld.add(key.data(), key.size(), hash_bytes(key.data(), key.size()), UINT32_MAX, r.lt,
+                    bld.node_id(r.node, r.node_len), r.voff, r.vlen);
+        } while (next_record(p));
+        closed = true;
+        p0.i = p.i;
+    } else {
+        // find where the closing '}' left the parse: the last used chunk's stop
+        for (int k = 0; k < n; ++k)
+            if (ch[k].closed) { p0.i = ch[k].stop; break; }
+    }
+    p0.ws();
+    if (p0.i != len) throw JsonError();
+    return CRDT_HOST_OK;
+}
+
+int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
+    const uint64_t n0 = keys->size();
+    try {
+        const int nt = len >= parallel_min_bytes() ? host_threads() : 1;
+        return nt > 1 ? decode_parallel(js, len, keys, d, nt) : decode_sequential(js, len, keys, d);
     } catch (const Fallback&) {
         crdt_keys_truncate(keys, n0);
         return CRDT_HOST_FALLBACK;
@@ -574,7 +833,6 @@ int decode(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded* d) {
         crdt_keys_truncate(keys, n0);
         return CRDT_HOST_E_NOMEM;
     }
-    return CRDT_HOST_OK;
 }
 
 }  // namespace

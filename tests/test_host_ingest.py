@@ -195,3 +195,68 @@ def test_hlc_format_matches_to_string(seed):
     with pytest.raises(hostlib.Fallback):                         # year 10000+: Dart's +YYYYYY form
         hostlib.hlc_strings(np.array([-(63_000_000_000_000 << 16)]), np.array([0], np.uint32), ["n"])
     assert iso_from_millis(-63_000_000_000_000).startswith("-0")
+
+
+# ------------------------------------------------------- parallel decode (large documents)
+def _decode_with(js, threads, par_min, pre=("k0",)):
+    old = {k: os.environ.get(k) for k in ("CRDT_HOST_THREADS", "CRDT_HOST_PAR_MIN")}
+    os.environ["CRDT_HOST_THREADS"] = str(threads)
+    os.environ["CRDT_HOST_PAR_MIN"] = str(par_min)
+    try:
+        keys = KeyIndex()
+        for k in pre:
+            keys.intern(k)
+        try:
+            dec = hostlib.decode(js, keys.native)
+        except hostlib.Fallback:
+            return "fallback", list(keys.keys)
+        except ValueError:
+            return "json", list(keys.keys)
+        cols = {k: np.asarray(v).tolist() for k, v in dec.items() if k not in ("buf", "nodes")}
+        return cols, dec["nodes"], list(keys.keys)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _adversarial_doc(rng, n):
+    """Records whose strings hold the `},"` split pattern, whitespace between tokens, escapes."""
+    hl = [str(Hlc(WALL + i, i % 7, f"n{i % 5}")) for i in range(50)]
+    parts = []
+    for i in range(n):
+        k = rng.choice(["k%d" % i, 'q},"%d' % i, "e\\u00e9%d" % i, "k%d" % (i // 3)])
+        v = rng.choice(['"},\\"x\\":{\\"hlc\\":\\""', '{"a": "},\\"b\\": 1"}', "[1, 2]", "null", '"plain"',
+                        '{"z":{"y":[{},{"x":"},"}]}}'])
+        ws = rng.choice(["", " ", "\n  "])
+        parts.append(f'{ws}"{k}"{ws}:{ws}{{"hlc":{ws}"{hl[i % 50]}",{ws}"value":{ws}{v}}}{ws}')
+    return "{" + ",".join(parts) + "}"
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_parallel_decode_equals_sequential(seed):
+    rng = np.random.default_rng(100 + seed)
+    js = _random_doc(rng, int(rng.integers(200, 1500))) if seed % 2 else _adversarial_doc(rng, int(rng.integers(200, 1500)))
+    want = _decode_with(js, 1, 1 << 60)
+    for threads in (2, 3, 7, 16):
+        assert _decode_with(js, threads, 0) == want, threads
+    if want[0] not in ("fallback", "json"):
+        keys = KeyIndex()
+        keys.intern("k0")
+        assert _native_records(hostlib.decode(js, keys.native), keys) == _python_records(js)
+
+
+@pytest.mark.parametrize("where", [0.1, 0.5, 0.9])
+def test_parallel_decode_errors_match_sequential(where):
+    rng = np.random.default_rng(7)
+    js = _random_doc(rng, 800, dup_frac=0.0)
+    cut = int(len(js) * where)
+    i = js.index('"hlc"', cut)
+    bad_hlc = js[:i] + '"hlc":"2021-01-01T00:00:00Z-0001-n","x' + js[i + 5:]     # fallback form
+    broken = js[:cut] + "}{" + js[cut:]                                          # malformed
+    for doc in (bad_hlc, broken, js[:-1], js + " x"):
+        want = _decode_with(doc, 1, 1 << 60)
+        for threads in (2, 5, 16):
+            assert _decode_with(doc, threads, 0) == want
