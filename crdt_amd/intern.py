@@ -229,8 +229,34 @@ class ValueStore:
             self._free.append(handle)
 
     def release_many(self, handles):
-        for h in handles:
-            self.release(int(h))
+        """release() of many handles at once (vectorised: a merge can drop millions of losers)."""
+        import numpy as np
+        h = np.asarray(handles, np.int64)
+        h = h[h != NULL_HANDLE]
+        if len(h) == 0:
+            return
+        if len(h) < 64:
+            for x in h.tolist():
+                self.release(x)
+            return
+        h = np.unique(h)
+        flags = np.frombuffer(bytes(self._rawflag), np.uint8)
+        raw = h[flags[h] == 1]
+        if len(raw):                                    # live-count bookkeeping of raw batches
+            starts = np.asarray(self._raw_start, np.int64)
+            bi = np.searchsorted(starts, raw, side="right") - 1
+            for b, cnt in zip(*np.unique(bi, return_counts=True)):
+                batch = self._raw[int(b)]
+                batch[3] -= int(cnt)
+                if batch[3] == 0:
+                    batch[0] = batch[1] = batch[2] = None
+        vals = self._values
+        for x in h.tolist():
+            vals[x] = None
+        rf = self._rawflag
+        for x in raw.tolist():
+            rf[x] = 0
+        self._free.extend(h.tolist())
 
     def compact(self, live_handles):
         """Free every handle not in ``live_handles``."""

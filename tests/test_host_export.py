@@ -170,3 +170,28 @@ def test_value_texts_reuse_raw_spans_and_match_dumps():
     hh = vs2.put_raw(buf, offs, lens)
     vs2.texts(hh, dumps)
     assert vs2._rawflag[int(hh[5])] == 1 and vs2._rawflag[int(hh[1])] == 0
+
+
+def test_release_many_equals_release_loop():
+    rng = np.random.default_rng(15)
+    stores = [ValueStore(), ValueStore()]
+    buf = b"".join(b'{"a":%d}' % i for i in range(500))
+    lens = np.full(500, 7, np.uint32)
+    lens[np.arange(500) >= 10] = [len(b'{"a":%d}' % i) for i in range(10, 500)]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    for vs in stores:
+        vs.put_raw(buf, offs, lens)
+        for i in range(300):
+            vs.put(i)
+        for h in range(0, 500, 7):
+            vs.get(h)                                   # some raw values decoded
+    drop = rng.choice(800, 400, replace=False).astype(np.uint32)
+    drop = np.concatenate([drop, [NULL_HANDLE]]).astype(np.uint32)
+    stores[0].release_many(drop)
+    for h in drop.tolist():
+        stores[1].release(h) if h != NULL_HANDLE else None
+    a, b = stores
+    assert a._values == b._values and bytes(a._rawflag) == bytes(b._rawflag)
+    assert sorted(a._free) == sorted(b._free)
+    assert [x[3] for x in a._raw] == [x[3] for x in b._raw]
+    assert [x[0] is None for x in a._raw] == [x[0] is None for x in b._raw]
