@@ -723,6 +723,25 @@ int host_threads() {
     return hc == 0 ? 1 : (hc < 16 ? (int)hc : 16);
 }
 
+// fn(chunk, begin, end) over [0, n) split into at most host_threads() chunks of >= min_per items
+// (the caller's thread runs chunk 0); returns the number of chunks.
+template <typename F>
+int parallel_chunks(uint64_t n, uint64_t min_per, F fn) {
+    int nt = host_threads();
+    if (const char* env = getenv("CRDT_HOST_MIN_CHUNK")) min_per = strtoull(env, nullptr, 10);   // tests
+    if (min_per == 0) min_per = 1;
+    if ((uint64_t)nt > n / min_per) nt = (int)std::max<uint64_t>(1, n / min_per);
+    const uint64_t per = (n + nt - 1) / std::max(nt, 1);
+    std::vector<std::thread> pool;
+    for (int k = 1; k < nt; ++k) {
+        const uint64_t b = std::min<uint64_t>(n, k * per), e = std::min<uint64_t>(n, b + per);
+        pool.emplace_back(fn, k, b, e);
+    }
+    fn(0, 0, std::min<uint64_t>(n, per));
+    for (auto& t : pool) t.join();
+    return nt;
+}
+
 uint64_t parallel_min_bytes() {                       // CRDT_HOST_PAR_MIN: tests split small documents
     if (const char* e = getenv("CRDT_HOST_PAR_MIN")) return strtoull(e, nullptr, 10);
     return 4ull << 20;
@@ -1158,14 +1177,19 @@ int crdt_hlc_format(const int64_t* lt, const uint32_t* node, uint64_t n, const c
 
 int crdt_json_canonical(const char* buf, const uint64_t* off, const uint32_t* len, uint64_t n, uint8_t* ok) {
     if ((!buf || !off || !len || !ok) && n) return CRDT_HOST_E_INVALID;
-    try {
-        for (uint64_t k = 0; k < n; ++k) {
-            Canon c{buf + off[k], len[k]};
-            ok[k] = len[k] > 0 && c.value(0) && c.i == c.n;
+    std::vector<int> st(64, CRDT_HOST_OK);
+    parallel_chunks(n, 16384, [&](int ch, uint64_t b, uint64_t e) {
+        try {
+            for (uint64_t k = b; k < e; ++k) {
+                Canon c{buf + off[k], len[k]};
+                ok[k] = len[k] > 0 && c.value(0) && c.i == c.n;
+            }
+        } catch (const std::bad_alloc&) {
+            st[ch] = CRDT_HOST_E_NOMEM;
         }
-    } catch (const std::bad_alloc&) {
-        return CRDT_HOST_E_NOMEM;
-    }
+    });
+    for (int v : st)
+        if (v != CRDT_HOST_OK) return v;
     return CRDT_HOST_OK;
 }
 
@@ -1207,39 +1231,57 @@ int crdt_json_encode(const crdt_keys* keys, const uint32_t* key_id, const int64_
     *out = nullptr;
     crdt_text* t = new (std::nothrow) crdt_text();
     if (!t) return CRDT_HOST_E_NOMEM;
-    try {
-        std::string& o = t->s;
-        uint64_t want = 2;
-        for (uint64_t i = 0; i < n; ++i) want += 64 + val_len[i];
-        o.reserve(want + want / 8);
-        o += '{';
-        char head[30];
-        for (uint64_t i = 0; i < n; ++i) {
-            const uint32_t id = key_id[i];
-            if (id >= keys->size() || node[i] >= n_nodes || (val_len[i] && (!val_txt || !val_txt[i]))) {
-                delete t;
-                return CRDT_HOST_E_INVALID;
-            }
-            if (i) o += ',';
-            o += '"';
-            json_escape(o, keys->arena.data() + keys->off[id], keys->off[id + 1] - keys->off[id]);
-            o += "\":{\"hlc\":\"";
-            if (hlc_txt && hlc_txt[i]) {                    // an Hlc not in columnar form (caller-made)
-                json_escape(o, hlc_txt[i], hlc_len[i]);
-            } else {
-                if (!hlc_head(lt[i], head)) {
-                    delete t;
-                    return CRDT_HOST_FALLBACK;
+    // records [b, e) into part `ch` (rows 1.. of a part start with ','), parts concatenated
+    std::vector<std::string> parts(64);
+    std::vector<int> st(64, CRDT_HOST_OK);
+    const int np = parallel_chunks(n, 32768, [&](int ch, uint64_t b, uint64_t e) {
+        try {
+            std::string& o = parts[ch];
+            uint64_t want = 0;
+            for (uint64_t i = b; i < e; ++i) want += 64 + val_len[i];
+            o.reserve(want + want / 8);
+            char head[30];
+            for (uint64_t i = b; i < e; ++i) {
+                const uint32_t id = key_id[i];
+                if (id >= keys->size() || node[i] >= n_nodes || (val_len[i] && (!val_txt || !val_txt[i]))) {
+                    st[ch] = CRDT_HOST_E_INVALID;
+                    return;
                 }
-                o.append(head, 30);
-                json_escape(o, node_buf + node_off[node[i]], node_off[node[i] + 1] - node_off[node[i]]);
+                if (i) o += ',';
+                o += '"';
+                json_escape(o, keys->arena.data() + keys->off[id], keys->off[id + 1] - keys->off[id]);
+                o += "\":{\"hlc\":\"";
+                if (hlc_txt && hlc_txt[i]) {                // an Hlc not in columnar form (caller-made)
+                    json_escape(o, hlc_txt[i], hlc_len[i]);
+                } else {
+                    if (!hlc_head(lt[i], head)) {
+                        st[ch] = CRDT_HOST_FALLBACK;
+                        return;
+                    }
+                    o.append(head, 30);
+                    json_escape(o, node_buf + node_off[node[i]], node_off[node[i] + 1] - node_off[node[i]]);
+                }
+                o += "\",\"value\":";
+                if (val_len[i]) o.append(val_txt[i], val_len[i]);
+                else o += "null";
+                o += '}';
             }
-            o += "\",\"value\":";
-            if (val_len[i]) o.append(val_txt[i], val_len[i]);
-            else o += "null";
-            o += '}';
+        } catch (const std::bad_alloc&) {
+            st[ch] = CRDT_HOST_E_NOMEM;
         }
-        o += '}';
+    });
+    for (int k = 0; k < np; ++k)
+        if (st[k] != CRDT_HOST_OK) {
+            delete t;
+            return st[k];
+        }
+    try {
+        uint64_t total = 2;
+        for (int k = 0; k < np; ++k) total += parts[k].size();
+        t->s.reserve(total);
+        t->s += '{';
+        for (int k = 0; k < np; ++k) t->s += parts[k];
+        t->s += '}';
     } catch (const std::bad_alloc&) {
         delete t;
         return CRDT_HOST_E_NOMEM;

@@ -195,3 +195,29 @@ def test_release_many_equals_release_loop():
     assert sorted(a._free) == sorted(b._free)
     assert [x[3] for x in a._raw] == [x[3] for x in b._raw]
     assert [x[0] is None for x in a._raw] == [x[0] is None for x in b._raw]
+
+
+def test_parallel_export_equals_sequential(monkeypatch):
+    """crdt_json_encode / crdt_json_canonical split over threads give the same bytes / flags."""
+    rng = np.random.default_rng(16)
+    ki = KeyIndex()
+    keys = [f"k{i}\t{'é' * (i % 3)}" for i in range(3000)]
+    ids = np.array([ki.intern(k) for k in keys], np.uint32)
+    n = len(keys)
+    lt = (rng.integers(0, 100_000_000_000_000, n) << 16) + rng.integers(0, 0x10000, n)
+    node = rng.integers(0, 3, n).astype(np.uint32)
+    vs = ValueStore()
+    handles = np.array([vs.put(_random_value(rng)) for _ in range(n)], np.uint32)
+    texts = [dumps(_random_value(rng)) for _ in range(n)]
+    monkeypatch.setenv("CRDT_HOST_THREADS", "1")
+    ptr, ln, keep = vs.texts(handles, dumps)
+    want = hostlib.encode(ki.native, ids, lt, node, ["a", "b\"", "c"], ptr, ln)
+    want_ok = _canon(texts)
+    monkeypatch.setenv("CRDT_HOST_THREADS", "7")
+    monkeypatch.setenv("CRDT_HOST_MIN_CHUNK", "100")
+    assert hostlib.encode(ki.native, ids, lt, node, ["a", "b\"", "c"], ptr, ln) == want
+    assert np.array_equal(_canon(texts), want_ok)
+    bad = lt.copy()
+    bad[2500] = -100_000_000_000_000 << 16                        # year < 0 in a later chunk
+    with pytest.raises(hostlib.Fallback):
+        hostlib.encode(ki.native, ids, bad, node, ["a", "b\"", "c"], ptr, ln)
