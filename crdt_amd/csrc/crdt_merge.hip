@@ -893,6 +893,7 @@ struct crdt_ctx {
     bool last_sorted = false;       // the last crdt_merge ran the sorted path
     bool fused = false;             // this plan: tile max in k_clock<true>, resolve in k_verify<true>
     bool scan_eager = false;        // next k_scan loads rank / millis with lt (last call: mostly hot tiles)
+    bool no_fuse = false;           // CRDT_NO_FUSE: small merges keep k_tmax / k_resolve_local / k_resolve
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
 };
@@ -1041,7 +1042,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
                                                                                      INT64_MIN);
     c->plan_R = R;
     c->plan_tiles = tiles;
-    c->fused = allow_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
+    c->fused = allow_fuse && !c->no_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
         const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
@@ -1471,6 +1472,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (const char* e = getenv("CRDT_MERGE_PATH")) {
         c->merge_path = strcmp(e, "gather") == 0 ? 1 : strcmp(e, "sorted") == 0 ? 2 : 0;
     }
+    if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
         const int v = atoi(e);
         c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;

@@ -76,6 +76,33 @@ def test_random_small(gpu_device, seed):
     compare_with_oracle(make_case(**kw))
 
 
+def _fused_cases():
+    yield make_case(seed=3100, R=7, per_cs=3000, n_local=5000, n_new=2000, millis_span=40, counter_span=3,
+                    n_ranks=9, dup_frac=0.002, drift_frac=0.002, local_rank=2)
+    yield make_case(seed=3101, R=2, per_cs=200_000, n_local=300_000, n_new=100_000,
+                    force=[(1, 150_001, "drift")], millis_span=1 << 12)
+    yield make_case(seed=3102, R=40, per_cs=500, n_local=8000, n_new=4000, millis_span=5, counter_span=2,
+                    n_ranks=41, force=[(33, 17, "dup")], local_rank=0)
+    yield make_case(seed=3103, R=1, per_cs=300_000, n_local=200_000, n_new=200_000, millis_span=1 << 14)
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_fused_small_merge_equals_unfused(gpu_device, monkeypatch, k):
+    """crdt_merge's fused form (tile max inside k_clock<true>, resolve by the last k_verify<true>
+    workgroup) against the separate kernels (CRDT_NO_FUSE) and the oracle."""
+    case = list(_fused_cases())[k]
+    fused = device_run(case)
+    monkeypatch.setenv("CRDT_NO_FUSE", "1")
+    plain = device_run(case)
+    for a, b in zip(fused[0], plain[0]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(fused[2], plain[2])
+    for f in RESULT_FIELDS:
+        assert fused[1][f] == plain[1][f], f
+    monkeypatch.delenv("CRDT_NO_FUSE")
+    compare_with_oracle(case)
+
+
 def test_device_resident_columns(gpu_device):
     """Zero-copy path: torch CUDA tensors go straight to the kernels."""
     compare_with_oracle(make_case(seed=77, R=5, per_cs=3000, n_local=6000, n_new=3000), device_cols=True)
