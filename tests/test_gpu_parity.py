@@ -504,3 +504,41 @@ def test_sorted_equals_gather_fanin(gpu_device, K, total, R):
     for a, b in zip(ag, as_):
         assert np.array_equal(a, b)
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("inject", [None, "drift", "dup"])
+def test_streaming_deltas_one_ctx_vs_oracle(gpu_device, inject):
+    """cfg5's shape at small scale on one context: one crdt_merge per delta, so from the second
+    call on the scan takes its eager form (the previous call's tiles were mostly above C_0);
+    every call's result and win flags, and the final rows, against the C oracle."""
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_cfg5
+    from oracle.oracle_c import OracleTable
+    wl = gen_cfg5(device="cuda", K=200_000, n_delta=40_000, deltas=8, inject=inject, inject_at=(5, 39_000),
+                  step_ms=1000)
+    np_ = lambda t: t.cpu().numpy()  # noqa: E731
+    own = {k: np_(v) for k, v in wl["owned"].items()}
+    loc = {k: np_(v) for k, v in wl["local"].items()}
+    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+    o = OracleTable(wl["capacity"], 0, wl["c0"])
+    t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+    o.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+    t.canonical = wl["c0"]
+    offs = wl["owned_offsets"]
+    for d in range(wl["R"]):
+        b, e = int(offs[d]), int(offs[d + 1])
+        cols = [own[k][b:e] for k in ("key", "lt", "rank", "val")]
+        res, fl = t.merge(*cols, np.array([0, e - b], np.uint64), int(wl["walls"][d]))
+        ores, ofl = o.merge(cols[0].astype(np.uint32), cols[1], cols[2].astype(np.uint32),
+                            cols[3].astype(np.uint32), np.array([0, e - b], np.uint64), int(wl["walls"][d]))
+        ores = ores.as_dict()
+        for f in RESULT_FIELDS:
+            assert res[f] == ores[f], (d, f, res[f], ores[f])
+        assert np.array_equal(fl, ofl), d
+        if res["status"] != 0:
+            break
+    lt, rank, val, mod = t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))
+    assert np.array_equal(lt, o.rows["lt"]) and np.array_equal(rank, o.rows["rank"])
+    assert np.array_equal(val, o.rows["val"]) and np.array_equal(mod, o.rows["mod"])
+    assert (res["status"] != 0) == (inject is not None)
+    t.close()
