@@ -542,3 +542,36 @@ def test_streaming_deltas_one_ctx_vs_oracle(gpu_device, inject):
     assert np.array_equal(val, o.rows["val"]) and np.array_equal(mod, o.rows["mod"])
     assert (res["status"] != 0) == (inject is not None)
     t.close()
+
+
+def _with_empty_changesets(case, every=3):
+    """Empty every changeset j with j % every != 0 (offsets repeat), keeping the rest as they were."""
+    offs = case["offsets"].astype(np.int64)
+    R = len(offs) - 1
+    keep = [j for j in range(R) if j % every == 0]
+    idx = np.concatenate([np.arange(offs[j], offs[j + 1]) for j in keep]) if keep else np.zeros(0, np.int64)
+    new = [0]
+    for j in range(R):
+        new.append(new[-1] + (int(offs[j + 1] - offs[j]) if j % every == 0 else 0))
+    for k in ("key", "lt", "rank", "val"):
+        case[k] = case[k][idx]
+    if case.get("millis") is not None:
+        case["millis"] = case["millis"][idx]
+    case["offsets"] = np.array(new, np.uint64)
+    return case
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_interleaved_empty_changesets(gpu_device, seed):
+    """Empty changesets between non-empty ones (zero tiles for them in the scan, the clock's
+    W-only steps, K2 skipping them), with an exception after some of them."""
+    case = make_case(seed=4200 + seed, R=30, per_cs=400, n_local=3000, n_new=1500, millis_span=30,
+                     counter_span=3, n_ranks=7, local_rank=1,
+                     force=[(21, 123, "drift")] if seed == 1 else [(27, 5, "dup")] if seed == 2 else [])
+    compare_with_oracle(_with_empty_changesets(case))
+
+
+def test_more_changesets_than_grid_rows(gpu_device):
+    """R = 70,000 changesets (> 65,535: the scan's grid.y loops; > the fused clock's limit)."""
+    compare_with_oracle(make_case(seed=4300, R=70_000, per_cs=2, n_local=300, n_new=200, millis_span=4000,
+                                  counter_span=2, n_ranks=9))
