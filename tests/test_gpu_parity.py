@@ -185,7 +185,15 @@ def test_reserve_preserves_rows(gpu_device):
     assert (lt[0], rank[0], val[0], mod[0]) == (42, 1, 7, 43) and mod[1] < 0
 
 
-def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home"):
+def _init_pg(dist, rank, world, backend):
+    import torch
+    if backend == "nccl":                      # RCCL: the collectives the bench runs at N > 1
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+
+
+def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home", backend="gloo"):
     import os
 
     import torch
@@ -195,7 +203,7 @@ def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home"):
     from crdt_amd.dist import route_by_owner, sharded_merge, sharded_merge_parts, torch_all_gather, torch_reducers
     from tests.test_dist_cpu import _parts_case, _split
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init_pg(dist, rank, world, backend)
     try:
         case = make_case(**case_kw) if protocol == "home" else _parts_case(case_kw, world)
         cap = -(-case["n_ids"] // world)
@@ -269,7 +277,7 @@ def test_two_rank_sharded_on_device(gpu_device, name, protocol):
     assert np.array_equal(flags, oflags)
 
 
-def _routed_gpu_worker(rank, world, port, case_kw, q):
+def _routed_gpu_worker(rank, world, port, case_kw, q, backend="gloo"):
     import os
 
     import torch
@@ -279,7 +287,7 @@ def _routed_gpu_worker(rank, world, port, case_kw, q):
     from crdt_amd.dist import sharded_merge_routed, torch_all_gather, torch_all_to_all, torch_alloc, torch_reducers
     from tests.test_dist_cpu import _home_batch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init_pg(dist, rank, world, backend)
     try:
         case = make_case(**case_kw)
         cap = -(-case["n_ids"] // world)
@@ -342,6 +350,39 @@ def test_two_rank_routed_on_device(gpu_device, name):
             assert np.array_equal(a[slots], orows[f][mine]), f
     assert tot == [ores["n_present"], ores["n_won"]]
     assert np.array_equal(flags, oflags)
+
+
+@pytest.mark.parametrize("protocol", ["home", "parts", "routed"])
+@pytest.mark.parametrize("name", ["r8_tombstones", "drift_late"])
+def test_rccl_single_rank_protocols(gpu_device, name, protocol):
+    """The three multi-GPU protocols over RCCL (backend ``nccl``) with one rank: the device-side
+    all-reduce / all-gather / all-to-all branches of crdt_amd/dist.py that the bench takes at N > 1
+    (the gloo tests above stage through the host)."""
+    import torch.multiprocessing as mp
+
+    from tests.test_dist_cpu import _free_port
+    kw = dict(CASE_SPECS)[name]
+    case = make_case(**kw)
+    orows, ores, oflags = oracle_run(case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    if protocol == "routed":
+        p = ctx.Process(target=_routed_gpu_worker, args=(0, 1, port, kw, q, "nccl"))
+    else:
+        p = ctx.Process(target=_sharded_gpu_worker, args=(0, 1, port, kw, q, protocol, "nccl"))
+    p.start()
+    rank, res, lt, rk, val, mod, sel, fl = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter",
+              "n_present", "n_won"):
+        assert res[f] == ores[f], (name, protocol, f)
+    flags = np.zeros(len(case["key"]), np.uint8)
+    flags[sel] = fl
+    assert np.array_equal(flags, oflags)
+    for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+        assert np.array_equal(a, orows[f]), f
 
 
 def test_route_kernels_partition(gpu_device):
