@@ -295,10 +295,14 @@ def main():
         del flags
 
     # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
-    cpu = cpu_omp = None
+    cpu = cpu_omp = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
+        if job:                        # the census merged with win flags: redo the timed path's merge
+            reset()
+            step()
+            torch.cuda.synchronize()
         cpu = cpu_baseline(wl, args.cpu_seconds)
-        cpu_omp = cpu_baseline_omp(wl, args.cpu_seconds)
+        cpu_omp, parity = cpu_baseline_omp(wl, args.cpu_seconds, table)
 
     out = {
         "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
@@ -309,7 +313,7 @@ def main():
                    "parallelism": (f"keyshard{world}-{'routed' if route else 'parts' if weak else 'home'}"
                                    if world > 1 else "single"), "merge_path": path,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
-        "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp,
+        "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp, "parity": parity,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
                          "apply_kernels_est": round(avg_launch_us * launches_per_step / 1e3, 3),
                          "apply_launches": launches_per_step,
@@ -318,6 +322,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     table.close()
+    if parity is not None and not parity["equal"]:
+        log(f"PARITY FAILURE against the CPU oracle: {parity}")
+        sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
 
@@ -358,9 +365,13 @@ def cpu_baseline(wl, budget_s):
                       f"merge, map_crdt.dart:43; one clock read per record, hlc.dart:82), {el:.1f}s"}
 
 
-def cpu_baseline_omp(wl, budget_s):
+def cpu_baseline_omp(wl, budget_s, table=None):
     """Times oracle/merge_omp.c (the optimised multi-core merge, same results) on the leading
-    changesets of the same workload, 16 changesets per call, within ~budget_s seconds."""
+    changesets of the same workload, 16 changesets per call, within ~budget_s seconds.
+
+    When the sample covers the whole batch, the oracle's final state is also the full-size parity
+    check of the GPU ``table`` (left by the timed path's last merge): every one of its rows and the
+    canonical clock, bit for bit.  Returns (baseline, parity or None)."""
     import torch
     from oracle.oracle_c import OracleTable
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
@@ -386,12 +397,31 @@ def cpu_baseline_omp(wl, budget_s):
         assert res.status == 0
         done = j1
         recs += e - b
+    parity = None
+    if table is not None and done == wl["R"]:
+        parity = full_parity(table, t, wl["capacity"])
     del t
     torch.cuda.synchronize()
-    return {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
-                      f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
-                      f"{threads} OpenMP threads, {el:.1f}s"}
+    return ({"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
+             "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
+                       f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
+                       f"{threads} OpenMP threads, {el:.1f}s"}, parity)
+
+
+def full_parity(table, oracle, cap: int, chunk: int = 1 << 25) -> dict:
+    """Every row of the GPU table (lt, rank, val, mod) and its canonical clock against the oracle's."""
+    ts = time.perf_counter()
+    bad = 0
+    for b in range(0, cap, chunk):
+        e = min(b + chunk, cap)
+        got = table.read_rows(np.arange(b, e, dtype=np.uint32))
+        ref = oracle.rows[b:e]
+        for f, a in zip(("lt", "rank", "val", "mod"), got):
+            bad += int(np.count_nonzero(a != ref[f]))
+    canon = table.canonical == oracle.canonical
+    return {"rows": cap, "fields_differing": bad, "canonical_equal": canon, "equal": bad == 0 and canon,
+            "against": "oracle/merge_omp.c final state (tests pin it to oracle/merge_oracle.c)",
+            "seconds": round(time.perf_counter() - ts, 1)}
 
 
 if __name__ == "__main__":
