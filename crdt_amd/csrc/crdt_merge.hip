@@ -1283,20 +1283,22 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         const uint32_t* rv = two ? c->p2_kj.p : c->p1_kj.p;
         const uint32_t max_items = nb + (uint32_t)(nw / kRPart) + 1;
         const size_t ksn = (size_t)(2 * (nw / kRPart) + 2) * kSKeys;     // part-state slots of split buckets
-        HIPALLOC(c->p_ibase.ensure(2 * (nb + 1)));
+        const uint32_t max_hot = std::min<uint32_t>(nb, (uint32_t)(nw / kRPart) + 1);   // split buckets hold > kRPart
+        HIPALLOC(c->p_ibase.ensure(2 * (nb + 1) + 1 + max_hot));
         HIPALLOC(c->p_kslt.ensure(2 * ksn));
         HIPALLOC(c->p_ksu32.ensure(6 * ksn));
         uint32_t* d_ib = c->p_ibase.p;
         uint32_t* d_hb = c->p_ibase.p + nb + 1;
+        uint32_t* d_hot = c->p_ibase.p + 2 * (nb + 1);                           // [0] count, [1..] buckets
         KeyState ps{c->p_kslt.p, c->p_ksu32.p, c->p_ksu32.p + ksn, c->p_ksu32.p + 2 * ksn};
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
-        k_bucket_items<<<1, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb);
+        k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
         k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv, c->table,
                                                                 c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
-        k_part_carry<<<dim3(kSKeys / 256, nb), 256, 0, c->stream>>>(bst, d_ib, d_hb, nb, c->table, c->cap, ps, cy);
+        k_part_carry<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table, c->cap, ps, cy);
         k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                  c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
         HIPCHK(hipGetLastError());
