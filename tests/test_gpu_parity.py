@@ -490,6 +490,34 @@ def test_sorted_split_hot_bucket(gpu_device):
     assert res["path"] == "sorted" and res["n_won"] > 0
 
 
+def _spread_case(case, buckets, n_ids):
+    """Remap a case's key ids i -> buckets[i // 4096] * 4096 + i % 4096 on an n_ids table."""
+    from tests._cases import ABSENT_MOD
+    bk = np.asarray(buckets, np.int64)
+    remap = lambda k: (bk[k.astype(np.int64) // 4096] * 4096 + k.astype(np.int64) % 4096)  # noqa: E731
+    loc = case["local"]
+    ids = remap(np.arange(case["n_local"]))
+    local = {"lt": np.zeros(n_ids, np.int64), "rank": np.zeros(n_ids, np.uint32),
+             "val": np.zeros(n_ids, np.uint32), "mod": np.full(n_ids, ABSENT_MOD, np.int64)}
+    for f in local:
+        local[f][ids] = loc[f]
+    out = dict(case, n_ids=n_ids, n_local=n_ids, local=local)
+    out["key"] = remap(case["key"]).astype(np.uint32)
+    return out
+
+
+def test_sorted_split_buckets_across_blocks(gpu_device):
+    """Split (hot) buckets at bucket ids on both sides of the 1024-bucket blocks of the item
+    prefix and hot list (k_bucket_items), two-level capacity 2^24: ~80K records in each of
+    six buckets (two parts each), ties and tombstones."""
+    buckets = [3, 1023, 1024, 2047, 2048, 4095]
+    base = make_case(seed=86, R=40, per_cs=12_000, n_local=18_000, n_new=6 * 4096 - 18_000, millis_span=4,
+                     counter_span=3, n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    case = _spread_case(base, buckets, 1 << 24)
+    res = compare_with_oracle(case, path="sorted", flags=False)
+    assert res["path"] == "sorted" and res["n_won"] > 0
+
+
 def test_sorted_windows_and_late_exception(gpu_device):
     """More changesets than one 4096-changeset window; a drift record in changeset 4500
     stops the batch there (later windows and changesets untouched)."""
