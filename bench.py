@@ -63,6 +63,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
+    p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
     return p.parse_args()
 
 
@@ -303,6 +304,9 @@ def main():
             torch.cuda.synchronize()
         cpu = cpu_baseline(wl, args.cpu_seconds)
         cpu_omp, parity = cpu_baseline_omp(wl, args.cpu_seconds, table)
+    pcie = None
+    if rank == 0 and world == 1 and not args.no_pcie and not wl.get("per_call"):
+        pcie = host_input_rate(table, wl, reset)
 
     out = {
         "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
@@ -314,6 +318,7 @@ def main():
                                    if world > 1 else "single"), "merge_path": path,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp, "parity": parity,
+        "pcie_inclusive": pcie,
         "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
                          "apply_kernels_est": round(avg_launch_us * launches_per_step / 1e3, 3),
                          "apply_launches": launches_per_step,
@@ -406,6 +411,38 @@ def cpu_baseline_omp(wl, budget_s, table=None):
              "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
                        f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
                        f"{threads} OpenMP threads, {el:.1f}s"}, parity)
+
+
+def host_input_rate(table, wl, reset, max_records: int = 128 << 20) -> dict:
+    """The boundary as a dart:ffi caller uses it: columns in host memory, copied to the device
+    inside crdt_merge.  Times one merge of the leading changesets (<= max_records records) from
+    pageable numpy arrays and from pinned host tensors; reported beside `value`, never as it."""
+    import torch
+    offs, own = wl["owned_offsets"], wl["owned"]
+    j1 = int(np.searchsorted(offs, max_records, side="right")) - 1
+    j1 = max(1, min(j1, wl["R"]))
+    n = int(offs[j1])
+    sub = offs[:j1 + 1].astype(np.uint64)
+    cols = [own[k][:n].cpu() for k in ("key", "lt", "rank", "val")]
+    out = {"unit": "records/s", "records": n, "changesets": j1}
+    for kind in ("pageable", "pinned"):
+        hc = [c.clone() if kind == "pageable" else c.pin_memory() for c in cols]
+        # numpy views of the same memory (int32 columns viewed as uint32, so nothing is re-copied)
+        hc_np = [h.numpy().view(np.uint32) if h.dtype == torch.int32 else h.numpy() for h in hc]
+        best = None
+        for _ in range(2):
+            reset()
+            ts = time.perf_counter()
+            res, _ = table.merge(*hc_np, sub, wl["wall"], win_flags=False)
+            dt = time.perf_counter() - ts
+            assert res["status"] == 0, res
+            best = dt if best is None else min(best, dt)
+        out[kind] = round(n / best, 1)
+        out[kind + "_ms"] = round(best * 1e3, 2)
+        del hc, hc_np
+    out["sample"] = (f"first {j1} of {wl['R']} changesets ({n:,} records, {20 * n / 1e9:.2f} GB of columns) "
+                     f"merged from host buffers: crdt_merge copies them to HBM, then runs the same path")
+    return out
 
 
 def full_parity(table, oracle, cap: int, chunk: int = 1 << 25) -> dict:
