@@ -103,7 +103,9 @@ struct Misc {
     crdt_result result;    // filled by k_resolve
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
-};
+    unsigned long long pad16;  // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
+};                             // kernel (1112 B took an aligned fill plus a tail fill, ~5 us each)
+static_assert(sizeof(Misc) % 16 == 0, "Misc is memset as whole 16-B words");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef long long i64x2 __attribute__((ext_vector_type(2)));
@@ -866,6 +868,14 @@ struct crdt_ctx {
     DBuf<long long> d_candkey;
     // staging of host-memory batches
     DBuf<uint32_t> s_key, s_rank, s_val;
+    // crdt_merge of a host batch: key / val windows are copied on cstream while K2 runs on
+    // stream (apply_ranges); kv_key / kv_val = the caller's host columns still to copy
+    hipStream_t cstream = nullptr;
+    std::vector<hipEvent_t> cevents;
+    const uint32_t* kv_key = nullptr;
+    const uint32_t* kv_val = nullptr;
+    uint64_t kv_n = 0, kv_done = 0, kv_window = 4ull << 20;
+    uint32_t kv_win = 0;
     DBuf<int64_t> s_lt, s_millis, s_mod;
     DBuf<uint8_t> s_flags;
     DBuf<uint32_t> s_out;
@@ -1113,6 +1123,39 @@ int phase_resolve(crdt_ctx* c, long long* d_event) {
     return CRDT_OK;
 }
 
+// Windowed staging of a host batch's key / val columns (crdt_merge): window w = records
+// [w * kKvWindow, ...) is copied on cstream and stream waits for its event before the first K2
+// piece that reads it, so the copy of window w + 1 runs under K2 of window w.  (lt / rank are
+// staged in full before the scan, which needs every record.)
+// (c->kv_window records, default 4M = 32 MB of key + val, ~0.6 ms of PCIe; CRDT_KV_WINDOW: tests)
+
+int kv_copy_next(crdt_ctx* c) {
+    const uint64_t b = c->kv_done, e = std::min<uint64_t>(c->kv_n, b + c->kv_window);
+    if (c->kv_win >= c->cevents.size()) {
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->cevents.push_back(ev);
+    }
+    HIPCHK(hipMemcpyAsync(c->s_key.p + b, c->kv_key + b, (e - b) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          c->cstream));
+    HIPCHK(hipMemcpyAsync(c->s_val.p + b, c->kv_val + b, (e - b) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          c->cstream));
+    HIPCHK(hipEventRecord(c->cevents[c->kv_win], c->cstream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->cevents[c->kv_win], 0));
+    c->kv_win++;
+    c->kv_done = e;
+    return CRDT_OK;
+}
+
+// every remaining window (the sorted path reads the whole columns)
+int kv_copy_all(crdt_ctx* c) {
+    while (c->kv_key && c->kv_done < c->kv_n) {
+        int st = kv_copy_next(c);
+        if (st) return st;
+    }
+    return CRDT_OK;
+}
+
 // K2 over changeset ranges: changeset j's records are [beg[j], fin[j]) of the columns (host arrays).
 // n = length of the columns (win flags are indexed like them).
 int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint64_t* fin, uint64_t n, int32_t mem,
@@ -1138,11 +1181,22 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
     int64_t win_j = -1;
     uint32_t win_n = 0;
     for (uint32_t j = 0; j < R; ++j) {
-        const uint64_t b = beg[j], e = fin[j];
-        if (e == b) continue;
+      // one K2 launch per piece of the changeset inside one staged key / val window (the whole
+      // changeset when the columns are resident); a changeset's keys are distinct, so its
+      // pieces are independent and all use R_j
+      for (uint64_t pb = beg[j], pe; pb < fin[j]; pb = pe) {
+        pe = fin[j];
+        if (c->kv_key) {
+            while (c->kv_done <= pb) {
+                int st = kv_copy_next(c);
+                if (st) return st;
+            }
+            pe = std::min<uint64_t>(pe, c->kv_done);
+        }
+        const uint64_t b = pb, e = pe;
         // HIP-event timing of sampled windows of kTimingWindow back-to-back launches (one event
         // pair per window, so the events do not split the stream the rest of the time)
-        if (c->timing && (nl++ % kTimingStride) == 0 && win_j < 0) {
+        if (c->timing && b == beg[j] && (nl++ % kTimingStride) == 0 && win_j < 0) {
             win_j = j;
             win_n = 0;
             ev_record(c, ev_base + 1 + 2 * (size_t)j);
@@ -1169,6 +1223,7 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
             c->windows.push_back({(uint32_t)win_j, win_n});
             win_j = -1;
         }
+      }
     }
     if (win_j >= 0) {
         ev_record(c, ev_base + 2 + 2 * (size_t)win_j);
@@ -1376,7 +1431,10 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     Cols cols;
     if ((st = stage_apply_cols(c, owned, &cols))) return st;
     c->last_sorted = allow_sorted && use_sorted(c, owned, win_flags);
-    if (c->last_sorted) return apply_sorted(c, cols, owned->offsets, wall, d_event, out, ev_base);
+    if (c->last_sorted) {
+        if ((st = kv_copy_all(c))) return st;
+        return apply_sorted(c, cols, owned->offsets, wall, d_event, out, ev_base);
+    }
     return apply_ranges(c, cols, owned->offsets, owned->offsets + 1, owned->offsets[R], owned->mem, wall, d_event,
                         win_flags, out, ev_base);
 }
@@ -1475,6 +1533,10 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
         c->merge_path = strcmp(e, "gather") == 0 ? 1 : strcmp(e, "sorted") == 0 ? 2 : 0;
     }
     if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_KV_WINDOW")) {
+        const long long v = atoll(e);
+        if (v > 0) c->kv_window = (uint64_t)v;
+    }
     if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
         const int v = atoi(e);
         c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
@@ -1517,6 +1579,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->p_ibase.release(); c->p_ksu32.release(); c->p_kslt.release(); c->p_tseg.release();
     c->p_ibucket.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
+    for (hipEvent_t e : c->cevents) hipEventDestroy(e);
+    if (c->cstream) hipStreamDestroy(c->cstream);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1744,11 +1808,25 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     crdt_batch dev = *batch;
     uint8_t* dflags = win_flags;
     const uint64_t n = batch->offsets[R];
+    struct KvReset {                                         // no window outlives this call
+        crdt_ctx* c;
+        ~KvReset() { c->kv_key = c->kv_val = nullptr; c->kv_n = c->kv_done = 0; c->kv_win = 0; }
+    } kv_reset{c};
     if (batch->mem == CRDT_MEM_HOST) {
+        // lt / rank / millis now (the scan reads every record); key / val window by window
+        // under K2 on the copy stream (kv_copy_next)
+        if (n > 0 && (!batch->key_id || !batch->val)) return CRDT_E_INVALID;
         Cols cols;
-        if ((st = stage_apply_cols(c, batch, &cols))) return st;
-        if ((st = stage(c, c->s_millis, batch->millis, n, batch->mem, &cols.millis))) return st;
-        dev.key_id = cols.key; dev.lt = cols.lt; dev.rank = cols.rank; dev.val = cols.val;
+        if ((st = stage_check_cols(c, batch, &cols))) return st;
+        HIPALLOC(c->s_key.ensure(n ? n : 1));
+        HIPALLOC(c->s_val.ensure(n ? n : 1));
+        if (n) {
+            if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+            c->kv_key = batch->key_id;
+            c->kv_val = batch->val;
+            c->kv_n = n;
+        }
+        dev.key_id = c->s_key.p; dev.lt = cols.lt; dev.rank = cols.rank; dev.val = c->s_val.p;
         dev.millis = cols.millis;
         dev.mem = CRDT_MEM_DEVICE;
         if (win_flags) {

@@ -103,6 +103,20 @@ def test_fused_small_merge_equals_unfused(gpu_device, monkeypatch, k):
     compare_with_oracle(case)
 
 
+@pytest.mark.parametrize("window", [1, 777, 3000, 1 << 20])
+def test_host_batch_key_val_windows(gpu_device, monkeypatch, window):
+    """Host batches: key / val are staged window by window on the copy stream under K2
+    (CRDT_KV_WINDOW records per window; changesets split into pieces at window ends), with
+    win flags, a late duplicate-node exception and the sorted path, against the oracle."""
+    monkeypatch.setenv("CRDT_KV_WINDOW", str(window))
+    case = make_case(seed=3200, R=7, per_cs=3000, n_local=12_000, n_new=6000, millis_span=30, counter_span=3,
+                     n_ranks=9, local_rank=2)
+    compare_with_oracle(case)
+    compare_with_oracle(make_case(seed=3201, R=6, per_cs=2500, n_local=9000, n_new=4000, millis_span=20,
+                                  n_ranks=7, force=[(4, 1234, "dup")], local_rank=1))
+    compare_with_oracle(case, path="sorted", flags=False)
+
+
 def test_device_resident_columns(gpu_device):
     """Zero-copy path: torch CUDA tensors go straight to the kernels."""
     compare_with_oracle(make_case(seed=77, R=5, per_cs=3000, n_local=6000, n_new=3000), device_cols=True)
