@@ -140,7 +140,9 @@ constexpr uint32_t kHotSample = 16;              // tiles_hot counts every 16th 
 // kEager: rank / millis are loaded with lt instead of after it (one memory round trip per
 // tile instead of two) — chosen when the previous call found most tiles above C_0 (streaming
 // deltas); otherwise only waves holding such a record load them (the fan-in: ~none do).
-template <bool kEager>
+// kMillis: the batch carries an explicit millis column (an Hlc whose counter exceeds 0xFFFF);
+// without it millis = lt >> 16 and the eager form keeps no millis registers.
+template <bool kEager, bool kMillis = true>
 __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
@@ -160,14 +162,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         int f = 0;
         int64_t v[kScanItems];
         uint32_t rk[kEager ? kScanItems : 1];
-        int64_t mv[kEager ? kScanItems : 1];
+        int64_t mv[kEager && kMillis ? kScanItems : 1];
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
             v[q] = i < end ? lt[i] : INT64_MIN;
             if (kEager) {
                 rk[q] = i < end ? rank[i] : 0u;
-                mv[q] = (millis && i < end) ? millis[i] : 0;
+                if (kMillis) mv[kMillis ? q : 0] = (millis && i < end) ? millis[i] : 0;
             }
             m = imax(m, v[q]);
         }
@@ -176,7 +178,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         for (int q = 0; q < kScanItems; ++q) {
             if (v[q] > c0) {
                 const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-                const int64_t ms = millis ? (kEager ? mv[kEager ? q : 0] : millis[i]) : (v[q] >> kShift);
+                const int64_t ms = (kMillis && millis) ? (kEager ? mv[kEager && kMillis ? q : 0] : millis[i])
+                                                       : (v[q] >> kShift);
                 const uint32_t r = kEager ? rk[kEager ? q : 0] : rank[i];
                 f |= (r == local_rank) | (wsub(ms, wall) > kMaxDrift);
             }
@@ -1059,7 +1062,11 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (c->scan_eager)
+            if (c->scan_eager && !cols.millis)
+                k_scan<true, false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            else if (c->scan_eager)
                 k_scan<true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
