@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
+    p.add_argument("--exact-counts", action="store_true",
+                   help="per-record n_present / n_won also on the sorted path (its changeset-ordered form)")
     return p.parse_args()
 
 
@@ -145,6 +147,9 @@ def main():
 
     table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
     table.set_merge_path(args.path)
+    # per-record n_present / n_won are library extras (not reference results); without them the
+    # sorted path folds each bucket in any order (same rows / canonical / status)
+    table.set_counts(args.exact_counts)
     loc = wl["local"]
     own, home = wl["owned"], wl["home"]
     own_cols = (own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], None)
@@ -246,7 +251,8 @@ def main():
 
     # ---- per-kernel roofline of K2 (apply): algorithmic bytes / event-timed duration
     n_owned = int(res.get("n_recv", wl["owned_offsets"][-1]))            # routed: records received
-    kb = 20 * n_owned + 12 * res["n_present"] + 24 * res["n_won"]          # per step, this rank
+    counts_known = res["n_present"] != (1 << 64) - 1                       # order-free sorted path: not counted
+    kb = 20 * n_owned + (12 * res["n_present"] + 24 * res["n_won"] if counts_known else 0)   # per step, this rank
     launches_per_step = max(apply_total // max(args.steps, 1), 1)
     alg_per_launch = kb / launches_per_step
     avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)                  # HIP events, sampled launches
@@ -294,6 +300,13 @@ def main():
                "hbm_frac_job": round(b_alg / (ms_per_step / 1e3) / HBM_PEAK, 4),
                "records_won_total": int(r2["n_won"])}
         del flags
+        if not counts_known and apply_ms > 0:
+            # the sorted apply's bytes from the distinct-key counts (SURVEY 8(d)'s own terms)
+            alg_per_launch = b_alg / launches_per_step
+            achieved = alg_per_launch / (avg_launch_us / 1e6)
+            roofline.update({"achieved": round(achieved / 1e9, 1), "frac": round(achieved / HBM_PEAK, 4),
+                             "alg_bytes_per_launch": int(alg_per_launch),
+                             "alg_bytes": "20 B x records + 12 B x U_touch + 24 B x U_win (distinct keys)"})
 
     # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
     cpu = cpu_omp = parity = None

@@ -88,6 +88,7 @@ SIGNATURES = {
     "crdt_route_scatter": (_INT, [_P, _P, _U32, _P, _P, _P, _P, _P, _P]),
     "crdt_merge_apply_segments": (_INT, [_P, _P, _P, _P, _P, _U64, _P, _P, _I64, _P, _P, _P]),
     "crdt_set_merge_path": (_INT, [_P, _INT]),
+    "crdt_set_counts": (_INT, [_P, _INT]),
     "crdt_last_path": (_INT, [_P, _P]),
     "crdt_set_timing": (_INT, [_P, _INT]),
     "crdt_get_timing": (_INT, [_P, _P]),

@@ -904,6 +904,8 @@ struct crdt_ctx {
     DBuf<int64_t> p_kslt;
     HBuf<uint64_t> h_pplan;
     bool last_sorted = false;       // the last crdt_merge ran the sorted path
+    bool counts = true;             // crdt_set_counts: per-record n_present / n_won (the sorted path
+                                    // keeps changeset order for them; off -> its order-free form)
     bool fused = false;             // this plan: tile max in k_clock<true>, resolve in k_verify<true>
     bool scan_eager = false;        // next k_scan loads rank / millis with lt (last call: mostly hot tiles)
     bool no_fuse = false;           // CRDT_NO_FUSE: small merges keep k_tmax / k_resolve_local / k_resolve
@@ -1335,8 +1337,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
             k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
-            k_part_scatter2<<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p,
-                                                               c->p2_rec.p, c->p2_kj.p);
+            if (c->counts)
+                k_part_scatter2<true><<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits,
+                                                                        c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
+            else
+                k_part_scatter2<false><<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits,
+                                                                         c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
         }
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
         const uint32_t nb = two ? kDigits * kDigits : kDigits;
@@ -1358,11 +1364,23 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
-        k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv, c->table,
-                                                                c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
-        k_part_carry<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table, c->cap, ps, cy);
-        k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
-                                                                 c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
+        if (c->counts) {
+            k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
+                                                                    c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
+            k_part_carry<false><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table,
+                                                                                    c->cap, ps, cy, c->d_Rj.p, jb);
+            k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
+                                                                     c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
+        } else {        // order-free: no per-record counts; split buckets finished by k_part_carry<true>
+            k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
+                                                                          rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
+                                                                          c->d_misc);
+            k_part_carry<true><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table,
+                                                                                   c->cap, ps, cy, c->d_Rj.p, jb);
+            k_resolve<false, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
+                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
+                                                                           c->d_misc);
+        }
         HIPCHK(hipGetLastError());
     }
     if (c->timing) ev_record(c, ev_base + 2);
@@ -1404,8 +1422,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
     c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
     uint64_t np = 0, nw_ = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw_ += c->h_misc->won[s]; }
-    res.n_present = np;
-    res.n_won = nw_;
+    res.n_present = c->counts ? np : UINT64_MAX;       // the order-free form does not count them
+    res.n_won = c->counts ? nw_ : UINT64_MAX;
     if (c->h_misc->err) res.status = CRDT_E_KEY_RANGE;
     c->canonical = res.canonical_lt;
     if (out) *out = res;
@@ -1992,6 +2010,12 @@ int crdt_route_scatter(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, c
             out_rank, out_val, out_perm);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
+    return CRDT_OK;
+}
+
+int crdt_set_counts(crdt_ctx* c, int exact) {
+    if (!c || (exact != 0 && exact != 1)) return CRDT_E_INVALID;
+    c->counts = exact != 0;
     return CRDT_OK;
 }
 

@@ -274,6 +274,11 @@ class DeviceTable:
     # ---------------------------------------------------------------- timing
     PATHS = {"auto": 0, "gather": 1, "sorted": 2}
 
+    def set_counts(self, exact: bool):
+        """crdt_set_counts: per-record n_present / n_won; False lets the sorted path fold each
+        bucket in any order (same rows / canonical / status; both counts reported as 2^64 - 1)."""
+        self._check(self._lib.crdt_set_counts(self._ctx, 1 if exact else 0), "crdt_set_counts")
+
     def set_merge_path(self, path: str):
         """'auto' | 'gather' | 'sorted' (crdt_set_merge_path): the strategy of later merges."""
         self._check(self._lib.crdt_set_merge_path(self._ctx, self.PATHS[path]), "crdt_set_merge_path")

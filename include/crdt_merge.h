@@ -214,6 +214,13 @@ int crdt_merge_apply_segments(crdt_ctx* ctx, const uint32_t* key_id, const int64
  * crdt_merge took (CRDT_PATH_GATHER or CRDT_PATH_SORTED). */
 enum crdt_path { CRDT_PATH_AUTO = 0, CRDT_PATH_GATHER = 1, CRDT_PATH_SORTED = 2 };
 int crdt_set_merge_path(crdt_ctx* ctx, int path);
+
+/* Per-record counts (crdt_result.n_present / n_won): library extras, not part of the
+ * reference's merge (crdt.dart:77-94 exposes none).  exact = 1 (default): both paths count
+ * them.  exact = 0: when the sorted path runs it folds each bucket's records in any order
+ * (ties on (lt, rank) decided by changeset, the local row first — the same rows, canonical and
+ * status) and reports both counts as UINT64_MAX; the gather path still counts. */
+int crdt_set_counts(crdt_ctx* ctx, int exact);
 int crdt_last_path(const crdt_ctx* ctx, int* path);
 
 /* ---- measurement ---------------------------------------------------------- */

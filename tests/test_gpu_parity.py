@@ -12,13 +12,16 @@ RESULT_FIELDS = ("status", "n_stored", "exc_changeset", "exc_index", "canonical_
                  "n_present", "n_won")
 
 
-def device_run(case, device_cols=False, capacity=None, path=None, flags=True):
+def device_run(case, device_cols=False, capacity=None, path=None, flags=True, counts=True):
     """path: None (auto) | 'gather' | 'sorted' (crdt_set_merge_path); flags=False asks for no
-    per-record win flags (the sorted path's precondition), returned flags are then None."""
+    per-record win flags (the sorted path's precondition), returned flags are then None;
+    counts=False: crdt_set_counts(0) (the sorted path's order-free form)."""
     from crdt_amd import DeviceTable
     t = DeviceTable(0, local_rank=case["local_rank"], capacity=capacity or case["n_ids"])
     if path:
         t.set_merge_path(path)
+    if not counts:
+        t.set_counts(False)
     loc = case["local"]
     keep = loc["mod"] != ABSENT_MOD
     ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
@@ -59,6 +62,9 @@ def compare_with_oracle(case, **kw):
     if flags is not None:
         assert np.array_equal(flags, oflags)
     for k in RESULT_FIELDS:
+        if kw.get("counts", True) is False and res["path"] == "sorted" and k in ("n_present", "n_won"):
+            assert res[k] == (1 << 64) - 1, (k, res[k])
+            continue
         assert res[k] == ores[k], (k, res[k], ores[k])
     return res
 
@@ -451,18 +457,22 @@ def _sorted_expected(case):
 
 
 @pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
-def test_sorted_golden_vectors(gpu_device, name):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_golden_vectors(gpu_device, name, counts):
     case, exp, expected = golden_case(name)
-    rows, res, flags = device_run(case, path="sorted", flags=False)
+    rows, res, flags = device_run(case, path="sorted", flags=False, counts=counts)
     check_rows(*rows, exp)
     assert flags is None
     for k, v in expected.items():
+        if not counts and res["path"] == "sorted" and k in ("n_present", "n_won"):
+            continue
         assert res[k] == v, (name, k, res[k], v)
     assert res["path"] == _sorted_expected(case)
 
 
 @pytest.mark.parametrize("seed", range(12))
-def test_sorted_random_small(gpu_device, seed):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_random_small(gpu_device, seed, counts):
     rng = np.random.default_rng(1000 + seed)
     kw = dict(seed=2000 + seed, R=int(rng.integers(1, 12)), per_cs=int(rng.integers(0, 500)),
               n_local=int(rng.integers(1, 600)), n_new=int(rng.integers(0, 400)),
@@ -472,35 +482,38 @@ def test_sorted_random_small(gpu_device, seed):
               drift_frac=float(rng.random() * 0.005))
     kw["local_rank"] = int(rng.integers(0, kw["n_ranks"]))
     case = make_case(**kw)
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["path"] == _sorted_expected(case)
 
 
 @pytest.mark.parametrize("capacity", [None, (1 << 20) + 7, 1 << 24])
-def test_sorted_ties_many_changesets(gpu_device, capacity):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_ties_many_changesets(gpu_device, capacity, counts):
     """300 tie-heavy changesets (same key in many of them, equal (lt, rank) across them):
     one-level buckets (capacity <= 2^20) and two-level (capacity > 2^20)."""
     case = make_case(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8,
                      counter_span=4, n_ranks=301)
-    res = compare_with_oracle(case, path="sorted", flags=False, capacity=capacity)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts, capacity=capacity)
     assert res["path"] == "sorted" and res["n_won"] > 0
 
 
-def test_sorted_hot_keys_in_one_chunk(gpu_device):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_hot_keys_in_one_chunk(gpu_device, counts):
     """Few keys, many changesets: every 2048-record chunk holds dozens of records per key,
     so the in-chunk same-key lists are long (ordering inside a chunk)."""
     case = make_case(seed=83, R=400, per_cs=60, n_local=50, n_new=30, millis_span=3, counter_span=2,
                      n_ranks=7)
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["path"] == "sorted"
 
 
-def test_sorted_split_hot_bucket(gpu_device):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_split_hot_bucket(gpu_device, counts):
     """All keys in one 4096-key bucket, 240K records: the bucket is resolved as 4 parts
     (part folds, carries, per-part counts) — ties and tombstones across the part cuts."""
     case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
                      n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["path"] == "sorted" and res["n_won"] > 0
 
 
@@ -520,7 +533,8 @@ def _spread_case(case, buckets, n_ids):
     return out
 
 
-def test_sorted_split_buckets_across_blocks(gpu_device):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_split_buckets_across_blocks(gpu_device, counts):
     """Split (hot) buckets at bucket ids on both sides of the 1024-bucket blocks of the item
     prefix and hot list (k_bucket_items), two-level capacity 2^24: ~80K records in each of
     six buckets (two parts each), ties and tombstones."""
@@ -528,24 +542,26 @@ def test_sorted_split_buckets_across_blocks(gpu_device):
     base = make_case(seed=86, R=40, per_cs=12_000, n_local=18_000, n_new=6 * 4096 - 18_000, millis_span=4,
                      counter_span=3, n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
     case = _spread_case(base, buckets, 1 << 24)
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["path"] == "sorted" and res["n_won"] > 0
 
 
-def test_sorted_windows_and_late_exception(gpu_device):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_windows_and_late_exception(gpu_device, counts):
     """More changesets than one 4096-changeset window; a drift record in changeset 4500
     stops the batch there (later windows and changesets untouched)."""
     case = make_case(seed=84, R=5000, per_cs=20, n_local=3000, n_new=2000, millis_span=20,
                      force=[(4500, 7, "drift")])
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["status"] == 1 and res["exc_changeset"] == 4500 and res["path"] == "sorted"
 
 
-def test_sorted_large_single_changeset(gpu_device):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_large_single_changeset(gpu_device, counts):
     from tests._cases import WALL
     case = make_case(seed=78, R=1, per_cs=1_000_000, n_local=1_200_000, n_new=800_000,
                      millis_span=1 << 16, base=WALL - 70_000)
-    res = compare_with_oracle(case, path="sorted", flags=False)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=counts)
     assert res["status"] == 0 and res["path"] == "sorted"
 
 
@@ -560,7 +576,8 @@ def test_sorted_key_out_of_range(gpu_device):
 
 
 @pytest.mark.parametrize("K,total,R", [(1 << 20, 3_000_000, 64), (1 << 24, 8_000_000, 96)])
-def test_sorted_equals_gather_fanin(gpu_device, K, total, R):
+@pytest.mark.parametrize("counts", [True, False])
+def test_sorted_equals_gather_fanin(gpu_device, K, total, R, counts):
     """Full-table property check at a fan-in shape (Zipf keys, unique per replica, hot head):
     both paths from the same state give the same rows, canonical and counts."""
     import torch
@@ -573,6 +590,7 @@ def test_sorted_equals_gather_fanin(gpu_device, K, total, R):
     for path in ("gather", "sorted"):
         t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
         t.set_merge_path(path)
+        t.set_counts(counts)
         t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
         t.canonical = wl["c0"]
         res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
@@ -583,6 +601,9 @@ def test_sorted_equals_gather_fanin(gpu_device, K, total, R):
         t.close()
     (rg, ag), (rs, as_) = out["gather"], out["sorted"]
     for k in RESULT_FIELDS:
+        if not counts and k in ("n_present", "n_won"):
+            assert rs[k] == (1 << 64) - 1
+            continue
         assert rg[k] == rs[k], (k, rg[k], rs[k])
     for a, b in zip(ag, as_):
         assert np.array_equal(a, b)
