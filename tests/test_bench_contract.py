@@ -1,0 +1,45 @@
+"""bench.py's output contract on a small fan-in: one JSON line with the driver's keys, the
+roofline and cpu_baseline objects, and full-table parity against the OpenMP oracle.
+
+Runs bench.py as a child process (one extra GPU process) at 1/250 of the default size so it
+finishes in seconds; the default-size line is in profiles/r01_bench_default.json."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+
+
+def _run_bench(*extra):
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--records", "4000000", "--replicas", "16", "--keys", str(1 << 22), "--local", str(1 << 21),
+           "--cpu-seconds", "0.5", "--no-pcie", *extra]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["gather", "sorted"])
+def test_bench_line_contract(gpu_device, path):
+    d = _run_bench("--path", path)
+    for k in KEYS:
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["data"] == "synthetic"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["config"]["records"] == 4000000 and d["config"]["merge_path"] == path
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cb = d["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
+    assert d["parity"]["equal"] is True and d["parity"]["fields_differing"] == 0
