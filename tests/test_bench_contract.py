@@ -43,3 +43,23 @@ def test_bench_line_contract(gpu_device, path):
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert d["parity"]["equal"] is True and d["parity"]["fields_differing"] == 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_weak(gpu_device):
+    """The N > 1 bench path (parts protocol, weak scaling) with 2 ranks on one GPU over gloo:
+    the driver's N = 2..8 runs take the same code with RCCL, one GPU per rank."""
+    env = dict(os.environ, CRDT_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--records", "4000000", "--replicas", "16"]
+    # (default key space: torch.distributed.run's own parser takes `--local` for `--local-addr`)
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]                  # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "keyshard2-parts"
+    assert d["config"]["records"] == 2 * 4000000                  # weak: every rank its own part
+    assert d["value"] > 0 and d["ms_per_step"] > 0
