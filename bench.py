@@ -1,24 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X MapCrdt merge hot path (BASELINE.json metric).
 
-Metric: merged records/sec (whole job, all ranks) on the 1024-replica fan-in
-workload — 1B records, Zipf(0.8) keys over 2^28 ids, a 2^27-key local map —
-plus the HBM-roofline fraction of the dominant kernel (K2 apply) and of the
-whole job.  One "step" = one crdt_merge of the whole batch (R = 1024 sequential
-Crdt.merge calls, crdt.dart:77-94) with every input already resident in HBM.
+Metric: merged records/sec (whole job, all ranks) on north-star config 4 — 1B records =
+1024 replicas x 976,563, Zipf(0.8) keys over 2^28 ids, a 2^27-key local map — plus the
+HBM-roofline fraction of the job (B_alg = 20 B x records + 12 B x U_touch
++ 24 B x U_win over distinct keys, / step time / (N x 8 TB/s)).  One "step" = one
+crdt_merge of the whole batch (R = 1024 sequential Crdt.merge calls, crdt.dart:77-94)
+with every input already resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-N > 1, --scaling weak (default): the job is N x the single-GPU workload —
-N·1B records, keys over N·2^28 ids sharded key % N, N·2^27 local keys; every
-rank generates its own part (its 2^28 slots), changeset j is the rank-major
-concatenation of the ranks' parts of replica j.  Per changeset one all-gather
-of the part maxima (N x R int64) plus the MIN/MAX event reductions of
-crdt_amd/dist.py::sharded_merge_parts — no records cross xGMI.
---scaling strong: the total stays 1B, keys sharded key % N, changeset j homed on
-rank j % N (dist.py::sharded_merge, three int64 all-reduces).
-Collectives are torch.distributed "nccl" = RCCL over xGMI.
+N = 1: one ctx merges the whole batch.
+N > 1 (strong scaling, config 4): the SAME 1B records; replica j arrives whole on rank
+j % N, keys are owned by rank key % N.  Every rank's ctx is joined to an RCCL
+communicator (crdt_comm_init_rccl) and the step is one collective crdt_merge per rank:
+the library all-gathers the part maxima, reduces the first exception, routes every
+record to its owner in one grouped all-to-all over xGMI and applies what it owns
+(crdt_amd/csrc/comm_path.inc).  value = 1,000,000,512 / max-over-ranks step time.  The
+pre-sharded figure (every rank already holding exactly the records it owns: no record
+exchange) is reported beside it under "presharded".
 """
 from __future__ import annotations
 
@@ -35,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 TIMING_EVERY = 8           # streaming configs (one merge call per delta): HIP-event timing sampled
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_bench.json")    # rocprofv3 --pmc of the default command
 
 
 def log(*a):
@@ -54,13 +56,11 @@ def parse():
     p.add_argument("--local", type=int, default=1 << 27)
     p.add_argument("--zipf", type=float, default=0.8)
     p.add_argument("--order", choices=["shuffled", "ascending"], default="shuffled")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
-    p.add_argument("--route", action="store_true",
-                   help="N > 1: changeset j arrives whole on rank j %% N; records are routed to their owner "
-                        "with RCCL all-to-all inside the timed step (north star config 4)")
     p.add_argument("--path", choices=["auto", "gather", "sorted"], default="auto",
                    help="merge strategy (crdt_set_merge_path): gather = K2 per changeset, sorted = key-partitioned")
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    p.add_argument("--no-presharded", action="store_true", help="N > 1: skip the pre-sharded figure")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of each CPU baseline sample")
+    p.add_argument("--cpu-changesets", type=int, default=64, help="changesets of the faithful CPU port's sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
@@ -79,55 +79,43 @@ def main():
     local_rank %= max(torch.cuda.device_count(), 1)          # gloo rehearsal: several ranks per GPU
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    # CRDT_BENCH_BACKEND=gloo: rehearsal of N ranks on one GPU (RCCL needs one GPU per rank); the
+    # library then exchanges through dist.GlooComm (host-staged) instead of its RCCL communicator
+    backend = os.environ.get("CRDT_BENCH_BACKEND", "nccl")
     if world > 1:
-        # CRDT_BENCH_BACKEND=gloo: rehearsal of N ranks on one GPU (RCCL needs one GPU per rank)
-        backend = os.environ.get("CRDT_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    from crdt_amd.dist import (sharded_merge, sharded_merge_parts, sharded_merge_routed, torch_all_gather,
-                               torch_all_to_all, torch_alloc, torch_reducers)
-    if world > 1:
-        red_max, red_min = torch_reducers(dist)
-        gather = torch_all_gather(dist)
-        a2a = torch_all_to_all(dist)
-        alloc = torch_alloc(dev)
     from crdt_amd import DeviceTable
+    from crdt_amd.dist import GlooComm, attach_rccl
     from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
 
+    def all_max(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_sum(x: int) -> int:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return int(t.item())
+
     t0 = time.time()
-    weak = world > 1 and args.scaling == "weak"
-    route = world > 1 and args.route
-    if args.config == "fanin" and route:
-        m = world if weak else 1
-        wl = gen_fanin(total=args.records * m, R=args.replicas, K=args.keys * m, n_local=args.local * m,
-                       s=args.zipf, device=dev, order=args.order, rank=rank, world=world, route=True)
-        workload = (f"fanin routed x{world} ({'weak' if weak else 'strong'}): {wl['total']:,} records = "
-                    f"{wl['R']} replicas x {wl['n_per_replica']:,}, replica j on rank j % {world}, Zipf({args.zipf}) "
-                    f"keys over {m}·2^{int(np.log2(args.keys))} ids routed to owner key % {world} by RCCL "
-                    f"all-to-all, local map {m}·2^{int(np.log2(args.local))} keys")
-    elif args.config == "fanin" and weak:
-        # this rank's part: a full single-GPU fan-in over its own 2^28 slots (global key = slot*N + rank)
+    census = args.config == "fanin" and not args.no_census and world > 1      # N > 1: counted at generation
+    if args.config == "fanin":
         wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                       device=dev, order=args.order, rank=0, world=1, seed=0xC0FFEE04 + 7919 * rank)
-        c0 = torch.tensor([wl["c0"]], dtype=torch.int64, device=dev)
-        red_max(c0)                                               # refreshCanonicalTime of the whole map
-        wl["c0"] = int(c0.item())
-        cnt = torch.from_numpy(np.diff(wl["owned_offsets"].astype(np.int64))).to(dev)
-        allc = gather(cnt).cpu().numpy()
-        wl["index_base"] = allc[:rank].sum(axis=0) if rank else np.zeros(allc.shape[1], np.int64)
-        wl["total"] = int(allc.sum())
-        workload = (f"fanin weak x{world}: {wl['total']:,} records = {wl['R']} replicas x "
-                    f"{world * wl['n_per_replica']:,}, per rank Zipf({args.zipf}) keys over its 2^"
-                    f"{int(np.log2(args.keys))} slots of {world}·2^{int(np.log2(args.keys))} ids (key % N), "
-                    f"{args.order} order, local map {world}·2^{int(np.log2(args.local))} keys")
-    elif args.config == "fanin":
-        wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                       device=dev, order=args.order, rank=rank, world=world)
+                       device=dev, order=args.order, rank=rank, world=world, route=world > 1, census=census)
         workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
                     f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
-                    f"{args.order} order), local map 2^{int(np.log2(args.local))} keys, keys sharded key%N")
+                    f"{args.order} order), local map 2^{int(np.log2(args.local))} keys")
+        if world > 1:
+            workload += (f"; replica j arrives whole on rank j % {world}, keys owned by rank key % {world}, "
+                         f"records routed to their owner inside the step (one grouped all-to-all per step)")
     elif args.config == "cfg2":
         assert world == 1, "cfg2 is a single-GPU configuration"
         wl = gen_cfg2(device=dev)
@@ -150,17 +138,16 @@ def main():
     # per-record n_present / n_won are library extras (not reference results); without them the
     # sorted path folds each bucket in any order (same rows / canonical / status)
     table.set_counts(args.exact_counts)
+    if world > 1:
+        if backend == "nccl":
+            attach_rccl(table, dist)                 # RCCL communicator inside the ctx
+        else:
+            table.comm_init_ops(world, rank, GlooComm(dist))
     loc = wl["local"]
-    own, home = wl["owned"], wl["home"]
-    own_cols = (own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], None)
-    if route:
-        home_cols = (home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], None)
-    else:
-        home_cols = (own["key"][:0] if world > 1 else own["key"], home["lt"], home["rank"],
-                     own["val"][:0] if world > 1 else own["val"], wl["home_offsets"], None)
+    src = wl["home"] if world > 1 else wl["owned"]
+    offs = wl["home_offsets"] if world > 1 else wl["owned_offsets"]
+    cols = (src["key"], src["lt"], src["rank"], src["val"], offs)
     R = wl["R"]
-    d_max = torch.zeros(max(R, 1), dtype=torch.int64, device=dev)
-    d_ev = torch.zeros(4, dtype=torch.int64, device=dev)
 
     def reset():
         table.clear_rows(0, wl["capacity"])
@@ -170,7 +157,7 @@ def main():
 
     def step(flags=None):
         if wl.get("per_call"):                       # streaming: one crdt_merge per delta
-            offs, tot = wl["owned_offsets"], None
+            tot = None
             for d in range(wl["R"]):
                 b, e = int(offs[d]), int(offs[d + 1])
                 fl = False if flags is None else flags[b:e]
@@ -189,19 +176,8 @@ def main():
                 if r["status"] != 0:
                     break
             return tot
-        if world == 1:
-            res, _ = table.merge(*own_cols[:5], wl["wall"], win_flags=flags if flags is not None else False)
-            return res
-        if route:
-            return sharded_merge_routed(table, home_cols, wl["wall"], d_max, d_ev, red_max, red_min, gather,
-                                        a2a, rank, world, alloc, win_flags=flags)
-        if weak:
-            # per changeset: part scan -> all-gather maxima -> clock -> MIN(event) -> resolve -> MAX -> apply
-            return sharded_merge_parts(table, own_cols, wl["wall"], wl["index_base"], d_max, d_ev, gather,
-                                       red_max, red_min, rank, win_flags=flags)
-        # key-sharded: home scan -> MAX(M_j) -> clock -> MIN(event) -> resolve -> MAX(details) -> apply
-        return sharded_merge(table, home_cols, own_cols, wl["wall"], d_max, d_ev, red_max, red_min,
-                             win_flags=flags)
+        res, _ = table.merge(*cols, wl["wall"], win_flags=flags if flags is not None else False)
+        return res
 
     def barrier():
         if world > 1:
@@ -211,138 +187,186 @@ def main():
     # streaming deltas: the per-call column views and offsets are made once, outside the timed steps
     delta_cols = []
     if wl.get("per_call"):
-        offs = wl["owned_offsets"]
         for d in range(wl["R"]):
             b, e = int(offs[d]), int(offs[d + 1])
-            delta_cols.append((own["key"][b:e], own["lt"][b:e], own["rank"][b:e], own["val"][b:e],
+            delta_cols.append((src["key"][b:e], src["lt"][b:e], src["rank"][b:e], src["val"][b:e],
                                np.array([0, e - b], np.uint64)))
     table_timing = [False, []]                     # per-call timing records (streaming config)
+
+    def timed_run(steps):
+        step_ms, tsum, res = [], {}, None
+        table.set_timing(True)
+        table_timing[0] = True
+        for _ in range(steps):
+            reset()
+            barrier()
+            ts = time.perf_counter()
+            res = step()
+            barrier()
+            step_ms.append(all_max(time.perf_counter() - ts) * 1e3)       # max over ranks
+            tms, table_timing[1] = table_timing[1] or [table.timing()], []
+            tm = {k: sum(t[k] for t in tms) for k in tms[0]}
+            if wl.get("per_call"):                   # sampled calls -> per-step estimates
+                f = wl["R"] / len(tms)
+                for k in ("scan_ms", "clock_ms", "route_ms", "total_ms"):
+                    tm[k] *= f
+                tm["apply_total"] = int(round(tm["apply_total"] * f))
+            for k, v in tm.items():
+                tsum[k] = tsum.get(k, 0) + v
+        table.set_timing(False)
+        table_timing[0] = False
+        return step_ms, tsum, res
+
     for _ in range(args.warmup):
         reset()
         step()
-    table.set_timing(True)
-    table_timing[0] = True
-    step_ms, apply_ms, apply_launches, apply_total, scan_ms, clock_ms, dev_ms = [], 0.0, 0, 0, 0.0, 0.0, 0.0
-    res = None
-    for _ in range(args.steps):
-        reset()
-        barrier()
-        ts = time.perf_counter()
-        res = step()
-        barrier()
-        dt = time.perf_counter() - ts
-        if world > 1:
-            t = torch.tensor([int(dt * 1e9)], device=dev, dtype=torch.int64)
-            red_max(t)                                            # max over ranks (ns)
-            dt = float(t.item()) / 1e9
-        step_ms.append(dt * 1e3)
-        tms, table_timing[1] = table_timing[1] or [table.timing()], []
-        tm = {k: sum(t[k] for t in tms) for k in tms[0]}
-        if wl.get("per_call"):                   # sampled calls -> per-step estimates
-            f = wl["R"] / len(tms)
-            for k in ("scan_ms", "clock_ms", "total_ms"):
-                tm[k] *= f
-            tm["apply_total"] = int(round(tm["apply_total"] * f))
-        apply_ms += tm["apply_ms"]
-        apply_launches += tm["apply_launches"]
-        apply_total += tm["apply_total"]
-        scan_ms += tm["scan_ms"]
-        clock_ms += tm["clock_ms"]
-        dev_ms += tm["total_ms"]
-    table.set_timing(False)
-    table_timing[0] = False
+    step_ms, tsum, res = timed_run(args.steps)
     assert res["status"] == 0, res
     ms_per_step = float(np.mean(step_ms))
     total_records = wl["total"]
     value = total_records / (ms_per_step / 1e3)
-
-    # ---- per-kernel roofline of K2 (apply): algorithmic bytes / event-timed duration
-    n_owned = int(res.get("n_recv", wl["owned_offsets"][-1]))            # routed: records received
-    counts_known = res["n_present"] != (1 << 64) - 1                       # order-free sorted path: not counted
-    kb = 20 * n_owned + (12 * res["n_present"] + 24 * res["n_won"] if counts_known else 0)   # per step, this rank
-    launches_per_step = max(apply_total // max(args.steps, 1), 1)
-    alg_per_launch = kb / launches_per_step
-    avg_launch_us = apply_ms * 1e3 / max(apply_launches, 1)                  # HIP events, sampled launches
-    achieved = alg_per_launch / (avg_launch_us / 1e6) if apply_ms > 0 else 0.0
     path = table.last_path()
-    roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
-                "kernel": "k_apply (K2)" if path == "gather" else
-                "sorted apply: k_part_* x2 + k_resolve (one timed region per merge call)",
-                "avg_launch_us": round(avg_launch_us, 2),
-                "alg_bytes_per_launch": int(alg_per_launch), "launches_per_step": launches_per_step,
-                "launches_timed": apply_launches}
-    if path == "gather" and args.config == "fanin" and world == 1 and apply_ms > 0:
-        # K2 against the measured ceiling of its own access pattern: random 16-B row reads
-        # with 25 % of rows written back on a 2^28-row table (tools/ubench_rowwrite.hip)
-        rate = (n_owned / launches_per_step) / (avg_launch_us / 1e6)
-        roofline["pattern_ceiling"] = {"value": 30.4e9, "unit": "records/s", "achieved": round(rate, 1),
-                                       "frac": round(rate / 30.4e9, 3),
-                                       "source": "profiles/r01_ubench_rowwrite.txt"}
-    # traffic (PMC) is filled from the committed rocprofv3 --pmc pass of this command, when present
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_apply.json")
-    if os.path.exists(pmc) and world == 1 and args.config == "fanin":
+    K = args.steps
+
+    # ---- whole-job algorithmic bytes: distinct keys touched / won
+    job = {}
+    if not args.no_census and wl.get("per_call"):
+        # streaming: every call is its own merge, so U is counted per call (= its records)
+        reset()
+        r2 = step(flags=torch.zeros(max(total_records, 1), dtype=torch.uint8, device=dev))
+        u_touch, u_win = int(r2["n_present"]), int(r2["n_won"])
+        job["census"] = "per call: U_touch = records whose key was present, U_win = records stored"
+    elif not args.no_census and world == 1:
+        # U_touch: distinct batch keys present in the local map; U_win: distinct keys of the stored
+        # records (win flags of one untimed census merge) — bitmaps over the key space, in chunks
+        reset()
+        flags = torch.zeros(max(total_records, 1), dtype=torch.uint8, device=dev)
+        r2 = step(flags=flags)
+        seen = torch.zeros(wl["capacity"], dtype=torch.bool, device=dev)
+        won = torch.zeros(wl["capacity"], dtype=torch.bool, device=dev)
+        for b in range(0, total_records, 1 << 27):
+            k = src["key"][b:b + (1 << 27)].long()
+            seen[k] = True
+            won[k[flags[b:b + (1 << 27)].bool()]] = True
+            del k
+        present = torch.zeros(wl["capacity"], dtype=torch.bool, device=dev)
+        present[loc["slot"].long()] = loc["mod"] >= 0
+        u_touch, u_win = int((seen & present).sum().item()), int(won.sum().item())
+        del flags, seen, won, present
+        job["records_won_total"] = int(r2["n_won"])
+        job["census"] = ("U_touch = distinct batch keys present in the local map, U_win = distinct keys of the "
+                         "records stored (win flags of one untimed merge)")
+    elif census:
+        u_touch = all_sum(wl["u_touch"])
+        # U_win: rows the merge stamped — mod >= c0 after the timed merge, less the local rows
+        # whose lt (= mod) is c0 (the only local rows that can carry it): exact up to those few
+        since = table.modified_since(wl["capacity"], wl["c0"])
+        local_at_c0 = int((loc["mod"] == wl["c0"]).sum().item())
+        u_win = all_sum(len(since) - local_at_c0)
+        job["census"] = ("U_touch = distinct batch keys present in the local map (bitmap at generation), "
+                         "U_win = rows stamped by the merge (mod >= C_0, crdt_modified_since) less the local "
+                         "rows at C_0; both summed over ranks")
+    if "census" in job:
+        b_alg = 20 * total_records + 12 * u_touch + 24 * u_win
+        job.update({"U_touch": u_touch, "U_win": u_win, "B_alg_bytes": b_alg,
+                    "hbm_frac_job": round(b_alg / (ms_per_step / 1e3) / (world * HBM_PEAK), 4)})
+
+    # ---- roofline: the contract fraction of the whole step (B_alg / t / (N x 8 TB/s)); the
+    # dominant kernel's own per-launch figure beside it
+    apply_ms = tsum.get("apply_ms", 0.0)
+    apply_launches = max(int(tsum.get("apply_launches", 0)), 1)
+    launches_per_step = max(int(tsum.get("apply_total", 0)) // max(K, 1), 1)
+    avg_launch_us = apply_ms * 1e3 / apply_launches
+    roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": None,
+                "traffic": None,
+                "scope": "whole step: B_alg (SURVEY 8(d), distinct keys) / step time / N GPUs"}
+    if job:
+        ach = job["B_alg_bytes"] / (ms_per_step / 1e3) / world
+        roofline.update(achieved=round(ach / 1e9, 1), frac=round(ach / HBM_PEAK, 4))
+    if path == "gather" and apply_ms > 0 and res["n_present"] != (1 << 64) - 1:
+        # K2 per launch on its own records (20 B each + 12 B per present + 24 B per won record,
+        # counted per record, i.e. repeated writes of a key in several changesets included)
+        n_mine = int(offs[-1]) if world == 1 else None
+        if n_mine is not None:
+            kb = (20 * n_mine + 12 * res["n_present"] + 24 * res["n_won"]) / launches_per_step
+            roofline["dominant_kernel"] = {
+                "kernel": "k_apply (K2)", "avg_launch_us": round(avg_launch_us, 2), "launches_per_step":
+                launches_per_step, "alg_bytes_per_launch": int(kb),
+                "achieved_GBs": round(kb / (avg_launch_us / 1e6) / 1e9, 1),
+                "frac": round(kb / (avg_launch_us / 1e6) / HBM_PEAK, 4),
+                "note": "per-record bytes (a key written by several changesets counts each time)"}
+        if args.config == "fanin" and world == 1:
+            rate = (int(offs[-1]) / launches_per_step) / (avg_launch_us / 1e6)
+            roofline["self_ubench_ceiling"] = {
+                "what": "K2's rate against the builder's own microbenchmark of its access pattern "
+                        "(random 16-B row reads, 25 % written back, 2^28 rows) -- not a roofline",
+                "value": 30.4e9, "unit": "records/s", "achieved": round(rate, 1), "frac": round(rate / 30.4e9, 3),
+                "source": "profiles/r01_ubench_rowwrite.txt"}
+    elif path == "sorted" and apply_ms > 0:
+        roofline["dominant_kernel"] = {"kernel": "sorted apply: k_part_* x2 + k_resolve",
+                                       "apply_ms_per_step": round(apply_ms / K, 3)}
+    # traffic: HBM bytes per step from this round's rocprofv3 --pmc passes of this exact command
+    if os.path.exists(PMC_FILE) and args.config == "fanin" and world == 1:
         try:
-            roofline["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pm = json.load(open(PMC_FILE))
+            if pm.get("command_args") == pmc_args(args) and pm.get("merge_path") == path:
+                roofline["traffic"] = pm["hbm_bytes_per_step"]
+                roofline["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
         except Exception:  # noqa: BLE001
             pass
 
-    # ---- whole-job algorithmic bytes: distinct keys touched / won (one untimed census run)
-    job = {}
-    if not args.no_census and world == 1:
-        reset()
-        flags = torch.zeros(max(n_owned, 1), dtype=torch.uint8, device=dev)
-        r2 = step(flags=flags) if world == 1 else None
-        if wl.get("per_call"):      # every call is its own merge: U counted per call (= its records)
-            u_touch, u_win = int(r2["n_present"]), int(r2["n_won"])
-        else:
-            keys = own["key"]
-            all_keys = torch.unique(keys)
-            u_touch = int((all_keys < wl["n_local_rows"]).sum().item()) if args.config in ("fanin", "cfg3") \
-                else int((all_keys < wl["n_local"]).sum().item())
-            del all_keys
-            u_win = int(torch.unique(keys[flags[:n_owned].bool()]).numel())
-        b_alg = 20 * total_records + 12 * u_touch + 24 * u_win
-        job = {"U_touch": u_touch, "U_win": u_win, "B_alg_bytes": b_alg,
-               "hbm_frac_job": round(b_alg / (ms_per_step / 1e3) / HBM_PEAK, 4),
-               "records_won_total": int(r2["n_won"])}
-        del flags
-        if not counts_known and apply_ms > 0:
-            # the sorted apply's bytes from the distinct-key counts (SURVEY 8(d)'s own terms)
-            alg_per_launch = b_alg / launches_per_step
-            achieved = alg_per_launch / (avg_launch_us / 1e6)
-            roofline.update({"achieved": round(achieved / 1e9, 1), "frac": round(achieved / HBM_PEAK, 4),
-                             "alg_bytes_per_launch": int(alg_per_launch),
-                             "alg_bytes": "20 B x records + 12 B x U_touch + 24 B x U_win (distinct keys)"})
+    # ---- pre-sharded figure (N > 1): every rank already holds exactly what it owns
+    presharded = None
+    if world > 1 and args.config == "fanin" and not args.no_presharded:
+        del wl["home"], src, cols
+        torch.cuda.empty_cache()
+        pw = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                       device=dev, order=args.order, rank=rank, world=world, route=False)
+        po = pw["owned"]
+        cols = (po["key"], po["lt"], po["rank"], po["val"], pw["owned_offsets"])
+        table.set_presharded(True)
+        for _ in range(max(1, args.warmup)):
+            reset()
+            step()
+        p_ms, p_sum, p_res = timed_run(args.steps)
+        assert p_res["status"] == 0 and p_res["canonical_lt"] == res["canonical_lt"], (p_res, res)
+        pm_ = float(np.mean(p_ms))
+        presharded = {"value": round(total_records / (pm_ / 1e3), 1), "unit": "records/s",
+                      "ms_per_step": round(pm_, 3), "step_ms_all": [round(x, 3) for x in p_ms],
+                      "what": "same job, every record already on its owner (crdt_set_presharded): no record "
+                              "exchange, only the clock collectives"}
+        table.set_presharded(False)
 
-    # ---- CPU baseline (rank 0, N = 1): the C restatement of the reference algorithm
+    # ---- CPU baselines (rank 0, N = 1): the C restatement of the reference algorithm
     cpu = cpu_omp = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         if job:                        # the census merged with win flags: redo the timed path's merge
             reset()
             step()
             torch.cuda.synchronize()
-        cpu = cpu_baseline(wl, args.cpu_seconds)
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_changesets)
         cpu_omp, parity = cpu_baseline_omp(wl, args.cpu_seconds, table)
     pcie = None
     if rank == 0 and world == 1 and not args.no_pcie and not wl.get("per_call"):
         pcie = host_input_rate(table, wl, reset)
 
+    n = world
     out = {
         "metric": "merged records/sec (node) + % HBM roofline, 1B records x 1024 replicas",
-        "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 1), "unit": "records/s", "n_gpus": n, "steps": K,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak" if (world == 1 or weak) else "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
         "config": {"workload": workload, "records": total_records, "replicas": R,
-                   "parallelism": (f"keyshard{world}-{'routed' if route else 'parts' if weak else 'home'}"
-                                   if world > 1 else "single"), "merge_path": path,
+                   "parallelism": f"keyshard{n}-routed" if world > 1 else "single", "merge_path": path,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp, "parity": parity,
-        "pcie_inclusive": pcie,
-        "breakdown_ms": {"scan": round(scan_ms / args.steps, 3), "clock_verify_resolve": round(clock_ms / args.steps, 3),
+        "pcie_inclusive": pcie, "presharded": presharded,
+        "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
+                         "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),
+                         "route": round(tsum.get("route_ms", 0) / K, 3),
                          "apply_kernels_est": round(avg_launch_us * launches_per_step / 1e3, 3),
                          "apply_launches": launches_per_step,
-                         "device_total": round(dev_ms / args.steps, 3)},
+                         "device_total": round(tsum.get("total_ms", 0) / K, 3)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -354,11 +378,21 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(wl, budget_s):
-    """Times oracle/merge_oracle.c (faithful port: map copy per merge + clock read per record,
-    single thread) on the first changesets of the same workload, within ~budget_s seconds."""
+def pmc_args(args) -> list:
+    """The arguments that define the workload a committed PMC profile must match."""
+    return [args.config, args.records, args.replicas, args.keys, args.local, args.zipf, args.order, args.path,
+            bool(args.exact_counts)]
+
+
+def cpu_baseline(wl, budget_s, n_changesets=64):
+    """Times oracle/merge_oracle.c in faithful mode — the reference algorithm: a full recordMap()
+    copy of the map per merge (map_crdt.dart:43, on T threads: the only unordered part), the
+    recv loop with a clock read per record (hlc.dart:82) and the winner loop, sequential — on the
+    first ``n_changesets`` changesets of the same workload (stopping early past ~budget_s x 4),
+    in blocks of 8 changesets whose rates give the spread."""
     import torch
     from oracle.oracle_c import OracleTable
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
     loc = wl["local"]
     cap = wl["capacity"]
     t = OracleTable(cap, 0, wl["c0"])
@@ -367,27 +401,32 @@ def cpu_baseline(wl, budget_s):
                loc["mod"].cpu().numpy())
     offs = wl["owned_offsets"]
     own = wl["owned"]
-    done, recs, el = 0, 0, 0.0
-    rows_copied = 0
-    while done < wl["R"] and el < budget_s:
-        b, e = int(offs[done]), int(offs[done + 1])
-        sl = slice(b, e)
-        cols = [own[k][sl].cpu().numpy() for k in ("key", "lt", "rank", "val")]
+    want = min(n_changesets, wl["R"])
+    done, recs, el, blocks = 0, 0, 0.0, []
+    while done < want and el < 4 * budget_s:
+        j1 = min(done + 8, want)
+        b, e = int(offs[done]), int(offs[j1])
+        cols = [own[k][b:e].cpu().numpy() for k in ("key", "lt", "rank", "val")]
+        sub = (offs[done:j1 + 1] - offs[done]).astype(np.uint64)
+        wall = int(wl["walls"][done]) if wl.get("per_call") else wl["wall"]
         ts = time.perf_counter()
         res, _ = t.merge(cols[0].astype(np.uint32), cols[1], cols[2].astype(np.uint32),
-                         cols[3].astype(np.uint32), np.array([0, e - b], np.uint64),
-                         int(wl["walls"][done]) if wl.get("per_call") else wl["wall"], faithful=True,
-                         want_flags=False)
-        el += time.perf_counter() - ts
-        done += 1
+                         cols[3].astype(np.uint32), sub, wall, faithful=threads, want_flags=False)
+        dt = time.perf_counter() - ts
+        assert res.status == 0
+        el += dt
+        blocks.append((e - b) / dt)
+        done = j1
         recs += e - b
-        rows_copied += cap
     del t
     torch.cuda.synchronize()
-    return {"value": round(recs / el, 1), "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged into the full "
-                      f"{cap:,}-row map by oracle/merge_oracle.c in faithful mode (one full map copy per "
-                      f"merge, map_crdt.dart:43; one clock read per record, hlc.dart:82), {el:.1f}s"}
+    return {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
+            "spread": {"min": round(min(blocks), 1), "median": round(float(np.median(blocks)), 1),
+                       "max": round(max(blocks), 1), "blocks": len(blocks), "changesets_per_block": 8},
+            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records, {100 * recs / wl['total']:.1f} % of "
+                      f"the batch) merged into the full {cap:,}-row map by oracle/merge_oracle.c in faithful "
+                      f"mode: one full map copy per merge (map_crdt.dart:43) on {threads} threads, one clock "
+                      f"read per record (hlc.dart:82) and the recv / winner loops on one thread, {el:.1f}s"}
 
 
 def cpu_baseline_omp(wl, budget_s, table=None):

@@ -21,6 +21,7 @@ CRDT_E_HIP = -2
 CRDT_E_NOMEM = -3
 CRDT_E_KEY_RANGE = -4
 CRDT_E_NO_DEVICE = -5
+CRDT_E_COMM = -6
 
 CRDT_MEM_HOST = 0
 CRDT_MEM_DEVICE = 1
@@ -47,11 +48,31 @@ class CrdtResult(ctypes.Structure):
 class CrdtTiming(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("clock_ms", ctypes.c_double),
                 ("apply_ms", ctypes.c_double), ("apply_launches", ctypes.c_uint32),
-                ("apply_total", ctypes.c_uint32), ("total_ms", ctypes.c_double)]
+                ("apply_total", ctypes.c_uint32), ("total_ms", ctypes.c_double),
+                ("route_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
 
+
+# crdt_comm_ops callbacks (include/crdt_merge.h)
+ALL_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32,
+                                 ctypes.c_void_p)
+ALL_GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                 ctypes.c_void_p)
+ALL_TO_ALL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
+                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p)
+
+
+class CrdtCommOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("mem", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("all_reduce_i64", ALL_REDUCE_FN), ("all_gather_i64", ALL_GATHER_FN),
+                ("all_to_all_v", ALL_TO_ALL_FN)]
+
+
+COMM_ID_BYTES = 128
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -80,13 +101,12 @@ SIGNATURES = {
     "crdt_put_stamped": (_INT, [_P, _P, _P, _U64, _I64, _I32, _P]),
     "crdt_refresh_canonical": (_INT, [_P, _U64, _P]),
     "crdt_merge": (_INT, [_P, _P, _I64, _P, _P]),
-    "crdt_merge_scan": (_INT, [_P, _P, _I64, _P]),
-    "crdt_merge_clock": (_INT, [_P, _P, _I64, _P, _P, _P, _P]),
-    "crdt_merge_resolve": (_INT, [_P, _P, _P]),
-    "crdt_merge_apply": (_INT, [_P, _P, _I64, _P, _P, _P]),
-    "crdt_route_count": (_INT, [_P, _P, _U32, _P]),
-    "crdt_route_scatter": (_INT, [_P, _P, _U32, _P, _P, _P, _P, _P, _P]),
-    "crdt_merge_apply_segments": (_INT, [_P, _P, _P, _P, _P, _U64, _P, _P, _I64, _P, _P, _P]),
+    "crdt_comm_unique_id": (_INT, [_P]),
+    "crdt_comm_init_rccl": (_INT, [_P, _U32, _U32, _P]),
+    "crdt_comm_init_ops": (_INT, [_P, _U32, _U32, _P]),
+    "crdt_comm_info": (_INT, [_P, _P, _P]),
+    "crdt_comm_free": (_INT, [_P]),
+    "crdt_set_presharded": (_INT, [_P, _INT]),
     "crdt_set_merge_path": (_INT, [_P, _INT]),
     "crdt_set_counts": (_INT, [_P, _INT]),
     "crdt_last_path": (_INT, [_P, _P]),

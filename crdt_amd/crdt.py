@@ -371,7 +371,7 @@ class MapCrdt(Crdt):
         lt = np.empty(n_total, np.int64)
         rank = np.empty(n_total, np.uint32)
         val = np.empty(n_total, np.uint32)
-        millis = None
+        odd = []                  # (index, Hlc.millis) of Hlcs outside the (millis << 16) + counter form
         offsets = np.zeros(R + 1, np.uint64)
         newid_start = []
         items = []
@@ -385,13 +385,16 @@ class MapCrdt(Crdt):
                 rank[i] = self._nodes.rank(h.nodeId)
                 val[i] = self._values.put(rec.value)
                 if not h.is_canonical_form:
-                    if millis is None:
-                        millis = lt >> 16
-                    millis[i] = h.millis
+                    odd.append((i, h.millis))
                 items.append((key, rec))
                 i += 1
             offsets[j + 1] = i
         newid_start.append(len(self._keys))
+        millis = None
+        if odd:                   # built from the COMPLETE lt column, then the odd Hlcs patched in
+            millis = lt >> 16
+            for x, ms in odd:
+                millis[x] = ms
         self._reserve()
         res, flags = self._table.merge(kid, lt, rank, val, offsets, wall, millis=millis)
         stop = res["n_stored"]

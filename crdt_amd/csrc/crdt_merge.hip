@@ -17,7 +17,9 @@
 //   K2  k_apply    per changeset: gather the local row, (lt, rank) compare, store
 //                  winner {lt, rank, val, mod = R_j} (crdt.dart:83-90)
 //                  [HBM: 20 B/record stream + 32 B row gather/scatter]
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>      // comm_path.inc: types / prototypes only (librccl is dlopen-ed)
 
 #include <stdint.h>
 #include <stdio.h>
@@ -575,17 +577,18 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
 #include "sorted_path.inc"
 
 // =============================================================================
-// Routing (multi-GPU, records arrive on their changeset's home rank): partition a
-// batch by owner rank key % G into per-(owner, changeset) chunks of the send
-// columns, slot = key / G.  Order inside a chunk is not preserved (keys are
-// unique within a changeset, so K2 is order-independent inside one); the
-// optional perm column gives each sent record's index in the batch.
+// Routing (key-sharded ctx, comm_path.inc): partition this rank's part of every
+// changeset by owner rank key % G into per-(owner, changeset) chunks of the send
+// columns, owner-major then changeset order; slot = key / G.  Order inside a chunk is
+// free (keys are distinct within a changeset, so K2 / the resolve do not depend on
+// it); the optional perm column gives each sent record's index in the batch (win
+// flags come back through it).  counts / cursors: [G][R] words.
 // =============================================================================
 constexpr int kRouteMaxRanks = 1024;
 
 __global__ __launch_bounds__(kScanThreads) void k_route_count(
     const uint32_t* __restrict__ key, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
-    uint32_t jbase, uint32_t G, unsigned long long* __restrict__ counts)
+    uint32_t jbase, uint32_t R, uint32_t G, unsigned long long* __restrict__ counts)
 {
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     const uint32_t j = jbase + blockIdx.y;
@@ -595,14 +598,20 @@ __global__ __launch_bounds__(kScanThreads) void k_route_count(
         for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
         __syncthreads();
         const uint64_t base = beg + (uint64_t)t * kTile;
+        uint32_t k[kScanItems];
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {          // every load in flight before the first atomic
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            k[q] = i < end ? __builtin_nontemporal_load(key + i) : 0u;
+        }
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-            if (i < end) atomicAdd(&s_cnt[key[i] % G], 1u);
+            if (i < end) atomicAdd(&s_cnt[k[q] % G], 1u);
         }
         __syncthreads();
         for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
-            if (s_cnt[d]) atomicAdd(&counts[(uint64_t)j * G + d], (unsigned long long)s_cnt[d]);
+            if (s_cnt[d]) atomicAdd(&counts[(uint64_t)d * R + j], (unsigned long long)s_cnt[d]);
         __syncthreads();
     }
 }
@@ -610,7 +619,7 @@ __global__ __launch_bounds__(kScanThreads) void k_route_count(
 __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
-    uint32_t jbase, uint32_t G, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ o_slot,
+    uint32_t jbase, uint32_t R, uint32_t G, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ o_slot,
     int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank, uint32_t* __restrict__ o_val,
     uint64_t* __restrict__ o_perm)
 {
@@ -623,33 +632,89 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
         for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
         __syncthreads();
         const uint64_t base = beg + (uint64_t)t * kTile;
-        uint32_t dst[kScanItems], pos[kScanItems];
+        uint32_t k[kScanItems], dst[kScanItems], pos[kScanItems];
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-            if (i < end) {
-                dst[q] = key[i] % G;
-                pos[q] = atomicAdd(&s_cnt[dst[q]], 1u);
-            }
+            k[q] = i < end ? __builtin_nontemporal_load(key + i) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+            dst[q] = k[q] % G;
+            pos[q] = i < end ? atomicAdd(&s_cnt[dst[q]], 1u) : 0u;
         }
         __syncthreads();
         for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
-            s_base[d] = s_cnt[d] ? atomicAdd(&cursor[(uint64_t)j * G + d], (unsigned long long)s_cnt[d]) : 0;
+            s_base[d] = s_cnt[d] ? atomicAdd(&cursor[(uint64_t)d * R + j], (unsigned long long)s_cnt[d]) : 0;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
             if (i < end) {
                 const uint64_t o = s_base[dst[q]] + pos[q];
-                o_slot[o] = key[i] / G;
-                o_lt[o] = lt[i];
-                o_rank[o] = rank[i];
-                o_val[o] = val[i];
+                o_slot[o] = k[q] / G;
+                o_lt[o] = __builtin_nontemporal_load(lt + i);
+                o_rank[o] = __builtin_nontemporal_load(rank + i);
+                o_val[o] = __builtin_nontemporal_load(val + i);
                 if (o_perm) o_perm[o] = i;
             }
         }
         __syncthreads();
     }
+}
+
+// Win flags of the sent records (send order, returned by the owners) -> batch order.
+__global__ __launch_bounds__(256) void k_flags_back(const uint8_t* __restrict__ sflags,
+                                                    const uint64_t* __restrict__ perm, uint64_t n,
+                                                    uint8_t* __restrict__ flags)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[perm[i]] = sflags[i];
+}
+
+// Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j.
+__global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict__ offs, uint32_t R,
+                                                     long long* __restrict__ gsend)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j < R) gsend[R + j] = (long long)(offs[j + 1] - offs[j]);
+}
+
+// From the all-gathered [G][2R] words (part maxima, part counts): M_j over all parts, and
+// for this rank's part the max / record count of the parts before it (lower ranks).
+__global__ __launch_bounds__(256) void k_shard_combine(const long long* __restrict__ g, uint32_t G, uint32_t me,
+                                                       uint32_t R, long long* __restrict__ M,
+                                                       long long* __restrict__ pbase,
+                                                       unsigned long long* __restrict__ ibase)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= R) return;
+    int64_t m = INT64_MIN, pm = INT64_MIN;
+    uint64_t ib = 0;
+    for (uint32_t r = 0; r < G; ++r) {
+        const int64_t v = g[(uint64_t)r * 2 * R + j];
+        m = imax(m, v);
+        if (r < me) {
+            pm = imax(pm, v);
+            ib += (uint64_t)g[(uint64_t)r * 2 * R + R + j];
+        }
+    }
+    M[j] = m;
+    pbase[j] = pm;
+    ibase[j] = ib;
+}
+
+// Per-record counts and the key-range error of this rank, as SUM-reducible words.
+__global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long long* __restrict__ out)
+{
+    if (threadIdx.x != 0) return;
+    unsigned long long np = 0, nw = 0;
+    for (int s = 0; s < kCounterSlots; ++s) { np += misc->present[s]; nw += misc->won[s]; }
+    out[0] = (long long)np;
+    out[1] = (long long)nw;
+    out[2] = misc->err ? 1 : 0;
+    out[3] = counted ? 0 : 1;
 }
 
 // ----------------------------------------------------------------- SPI kernels
@@ -845,6 +910,18 @@ struct HBuf {
     void release() { if (p) hipHostFree(p); p = nullptr; n = 0; }
 };
 
+// Changeset segments of the columns an apply phase reads, in changeset order: segment s is
+// records [beg[s], end[s]) of changeset j[s].  One per changeset for a local batch; one per
+// (changeset, source rank) for records routed in by a sharded merge.
+struct Segs {
+    std::vector<uint64_t> beg, end;
+    std::vector<uint32_t> j;
+    void from_offsets(const uint64_t* offs, uint32_t R) {
+        beg.resize(R); end.resize(R); j.resize(R);
+        for (uint32_t x = 0; x < R; ++x) { beg[x] = offs[x]; end[x] = offs[x + 1]; j[x] = x; }
+    }
+};
+
 }  // namespace
 
 struct crdt_ctx {
@@ -859,9 +936,6 @@ struct crdt_ctx {
     Misc* h_misc = nullptr;            // pinned
     DBuf<long long> d_M;               // [R]   (single-ctx merge)
     DBuf<long long> d_event;           // [4]
-    DBuf<uint64_t> d_rplan;            // routing: offsets + tile starts of the routed batch
-    HBuf<uint64_t> h_rplan;
-    DBuf<unsigned long long> d_rcount; // routing: [R][G] counts, then cursors
     DBuf<uint64_t> d_plan;             // offsets[R+1] (u64) then tile starts[R+1] (u32): one H2D copy
     HBuf<uint64_t> h_plan;
     const uint64_t* d_offs = nullptr;  // views into d_plan
@@ -884,15 +958,15 @@ struct crdt_ctx {
     DBuf<uint32_t> s_out;
     DBuf<long long> d_word;
     DBuf<unsigned long long> d_ibase;
-    HBuf<uint64_t> h_ibase;
     // per-call plan (set by scan, used by later phases)
     uint32_t plan_R = 0;
     uint64_t plan_tiles = 0;
+    uint32_t plan_mt = 0;           // most scan tiles of one changeset
     int apply_items = 0;            // K2 records per thread; 0 = by changeset size (CRDT_APPLY_ITEMS: tuning)
     // timing
     bool timing = false;
     std::vector<hipEvent_t> events;
-    std::vector<std::pair<uint32_t, uint32_t>> windows;   // timed (first changeset, launches)
+    std::vector<uint32_t> windows;  // launches of each timed apply window (events ev_window(k, *))
     uint32_t apply_total = 0;
     // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
     int merge_path = 0;
@@ -911,6 +985,22 @@ struct crdt_ctx {
     bool no_fuse = false;           // CRDT_NO_FUSE: small merges keep k_tmax / k_resolve_local / k_resolve
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
+    Segs segs;                      // changeset segments of the columns the apply phase reads
+    // key-sharded replica (comm_path.inc): this ctx is shard `rank` of `n_ranks`
+    uint32_t n_ranks = 1, rank = 0;
+    bool has_comm = false;
+    bool presharded = false;        // batches hold owned records only, key_id = slot
+    crdt_comm_ops ops{};            // the collective backend (RCCL: ops over rccl_comm)
+    void* rccl_comm = nullptr;
+    DBuf<long long> d_gsend, d_grecv, d_pbase, d_sum;
+    DBuf<unsigned long long> d_rcnt, d_rrecv;             // [G][R] route counts sent / received
+    HBuf<uint64_t> h_rcnt;                                // both, read back once per call
+    DBuf<uint32_t> r_skey, r_srank, r_sval, r_key, r_rank, r_val;   // send / receive columns
+    DBuf<int64_t> r_slt, r_lt;
+    DBuf<uint64_t> r_perm;
+    DBuf<uint8_t> r_flags, r_sflags;
+    HBuf<uint8_t> h_stage;                                // CRDT_MEM_HOST backends
+    HBuf<long long> h_sum;                                // reduced counts / error / uncounted
 };
 
 namespace {
@@ -1027,6 +1117,12 @@ int reset_misc(crdt_ctx* c) {
     return CRDT_OK;
 }
 
+// HIP events of a timed call: start, after the scan, after the clock phase (and its collectives),
+// apply start (route_ms = the gap before it), end; then one pair per sampled apply window.
+constexpr size_t kEvStart = 0, kEvScan = 1, kEvClock = 2, kEvApply = 3, kEvEnd = 4;
+inline size_t ev_window(size_t k, bool end) { return 5 + 2 * k + (end ? 1 : 0); }
+inline size_t events_for(size_t nsegs) { return ev_window(nsegs / kTimingStride + 2, true) + 1; }
+
 inline void ev_record(crdt_ctx* c, size_t idx) {
     if (c->timing && idx < c->events.size()) hipEventRecord(c->events[idx], c->stream);
 }
@@ -1057,6 +1153,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
                                                                                      INT64_MIN);
     c->plan_R = R;
     c->plan_tiles = tiles;
+    c->plan_mt = mt;
     c->fused = allow_fuse && !c->no_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
@@ -1084,8 +1181,11 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     return CRDT_OK;
 }
 
+// d_pbase / d_ibase_in (device, [R], optional): this ctx holds only a PART of each changeset,
+// preceded in its iteration order by parts whose max lt / record count these give (sharded merge).
 int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long long* d_maxima,
-                long long* d_event, const long long* d_pbase = nullptr, const uint64_t* h_ibase = nullptr) {
+                long long* d_event, const long long* d_pbase = nullptr,
+                const unsigned long long* d_ibase_in = nullptr) {
     const uint32_t R = c->plan_R;
     if (!home || home->n_changesets != R) return CRDT_E_INVALID;
     int st;
@@ -1094,14 +1194,7 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
     HIPALLOC(c->d_Cprev.ensure(R + 1));
     HIPALLOC(c->d_Rj.ensure(R + 1));
     HIPALLOC(c->d_Cj.ensure(R + 1));
-    const unsigned long long* d_ibase = nullptr;
-    if (h_ibase && R) {
-        HIPALLOC(c->d_ibase.ensure(R));
-        HIPALLOC(c->h_ibase.ensure(R));
-        memcpy(c->h_ibase.p, h_ibase, R * sizeof(uint64_t));
-        HIPCHK(hipMemcpyAsync(c->d_ibase.p, c->h_ibase.p, R * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-        d_ibase = c->d_ibase.p;
-    }
+    const unsigned long long* d_ibase = d_ibase_in;
     if (!R) k_event_init<<<1, 64, 0, c->stream>>>(d_event);   // else k_clock initialises the words
     if (c->fused) {                                           // (plan_tiles > 0, R <= kClockRMax)
         k_clock<true><<<1, 1024, 0, c->stream>>>(nullptr, c->d_T.p, c->d_tstart, R, wall, c->canonical,
@@ -1165,10 +1258,48 @@ int kv_copy_all(crdt_ctx* c) {
     return CRDT_OK;
 }
 
-// K2 over changeset ranges: changeset j's records are [beg[j], fin[j]) of the columns (host arrays).
-// n = length of the columns (win flags are indexed like them).
-int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint64_t* fin, uint64_t n, int32_t mem,
-                 int64_t wall, const long long* d_event, uint8_t* win_flags, crdt_result* out, size_t ev_base) {
+int comm_all_reduce(crdt_ctx* c, long long* d, uint64_t n, int32_t op);   // comm_path.inc
+
+// Read the call's outcome back (one D2H of Misc, the only sync of the apply phase).  On a
+// sharded ctx the per-record counts, the key-range error and "not counted" are SUM-reduced
+// over the ranks first, so every rank returns the same result.
+int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64_t n, bool sorted,
+                 crdt_result* out) {
+    const bool counted = !sorted || c->counts;          // the order-free sorted form does not count them
+    if (c->has_comm) {
+        HIPALLOC(c->d_sum.ensure(4));
+        HIPALLOC(c->h_sum.ensure(4));
+        k_sum_counts<<<1, 64, 0, c->stream>>>(c->d_misc, counted, c->d_sum.p);
+        int st = comm_all_reduce(c, c->d_sum.p, 4, CRDT_REDUCE_SUM);
+        if (st) return st;
+        HIPCHK(hipMemcpyAsync(c->h_sum.p, c->d_sum.p, 4 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+    if (host_flags && n) HIPCHK(hipMemcpyAsync(host_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    crdt_result res = c->h_misc->result;
+    c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
+    uint64_t np = 0, nw = 0;
+    for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
+    bool all_counted = counted, err = c->h_misc->err != 0;
+    if (c->has_comm) {
+        np = (uint64_t)c->h_sum.p[0];
+        nw = (uint64_t)c->h_sum.p[1];
+        err = c->h_sum.p[2] != 0;
+        all_counted = c->h_sum.p[3] == 0;
+    }
+    res.n_present = all_counted ? np : UINT64_MAX;
+    res.n_won = all_counted ? nw : UINT64_MAX;
+    if (err) res.status = CRDT_E_KEY_RANGE;
+    c->canonical = res.canonical_lt;
+    if (out) *out = res;
+    return res.status;
+}
+
+// K2 over the batch's changeset segments (host lists, changeset order; a changeset may be
+// several segments).  n = length of the columns (win flags are indexed like them).
+int apply_ranges(crdt_ctx* c, const Cols& cols, const Segs& sg, uint64_t n, int32_t mem,
+                 int64_t wall, const long long* d_event, uint8_t* win_flags, crdt_result* out) {
     const uint32_t R = c->plan_R;
     uint8_t* dflags = nullptr;
     if (win_flags) {
@@ -1183,18 +1314,19 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
     if (!c->resolved)
         k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     c->resolved = false;
-    ev_record(c, ev_base);
+    ev_record(c, kEvApply);
     c->windows.clear();
     uint32_t nl = 0;
     c->apply_total = 0;
-    int64_t win_j = -1;
+    bool win_open = false;
     uint32_t win_n = 0;
-    for (uint32_t j = 0; j < R; ++j) {
-      // one K2 launch per piece of the changeset inside one staged key / val window (the whole
-      // changeset when the columns are resident); a changeset's keys are distinct, so its
+    for (size_t s = 0; s < sg.j.size(); ++s) {
+      const uint32_t j = sg.j[s];
+      // one K2 launch per piece of the segment inside one staged key / val window (the whole
+      // segment when the columns are resident); a changeset's keys are distinct, so its
       // pieces are independent and all use R_j
-      for (uint64_t pb = beg[j], pe; pb < fin[j]; pb = pe) {
-        pe = fin[j];
+      for (uint64_t pb = sg.beg[s], pe; pb < sg.end[s]; pb = pe) {
+        pe = sg.end[s];
         if (c->kv_key) {
             while (c->kv_done <= pb) {
                 int st = kv_copy_next(c);
@@ -1205,10 +1337,10 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
         const uint64_t b = pb, e = pe;
         // HIP-event timing of sampled windows of kTimingWindow back-to-back launches (one event
         // pair per window, so the events do not split the stream the rest of the time)
-        if (c->timing && b == beg[j] && (nl++ % kTimingStride) == 0 && win_j < 0) {
-            win_j = j;
+        if (c->timing && b == sg.beg[s] && (nl++ % kTimingStride) == 0 && !win_open) {
+            win_open = true;
             win_n = 0;
-            ev_record(c, ev_base + 1 + 2 * (size_t)j);
+            ev_record(c, ev_window(c->windows.size(), false));
         }
         c->apply_total++;
         // records per thread (measured: more gathers in flight per thread beats more
@@ -1227,74 +1359,110 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const uint64_t* beg, const uint6
         else
             k_apply<1><<<grid, kApplyThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, b, e, j,
                                                               c->table, c->cap, c->d_Rj.p, c->d_misc, dflags);
-        if (win_j >= 0 && ++win_n == kTimingWindow) {
-            ev_record(c, ev_base + 2 + 2 * (size_t)win_j);
-            c->windows.push_back({(uint32_t)win_j, win_n});
-            win_j = -1;
+        if (win_open && ++win_n == kTimingWindow) {
+            ev_record(c, ev_window(c->windows.size(), true));
+            c->windows.push_back(win_n);
+            win_open = false;
         }
       }
     }
-    if (win_j >= 0) {
-        ev_record(c, ev_base + 2 + 2 * (size_t)win_j);
-        c->windows.push_back({(uint32_t)win_j, win_n});
+    if (win_open) {
+        ev_record(c, ev_window(c->windows.size(), true));
+        c->windows.push_back(win_n);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-    if (win_flags && mem == CRDT_MEM_HOST && n)
-        HIPCHK(hipMemcpyAsync(win_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    crdt_result res = c->h_misc->result;
-    c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
-    uint64_t np = 0, nw = 0;
-    for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
-    res.n_present = np;
-    res.n_won = nw;
-    if (c->h_misc->err) res.status = CRDT_E_KEY_RANGE;
-    c->canonical = res.canonical_lt;
-    if (out) *out = res;
-    return res.status;
+    return finish_apply(c, win_flags && mem == CRDT_MEM_HOST ? win_flags : nullptr, dflags, n, false, out);
 }
 
+#ifdef CRDT_PROF_RESOLVE
+// resolve phase clocks (CRDT_PROF_RESOLVE builds only)
+void prof_resolve_report() {
+        unsigned long long pr[8];
+        hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprof), sizeof(pr));
+        fprintf(stderr, "[rprof] items %llu chunks %llu | per item: init %.2f us final %.2f us | per chunk: "
+                "A %.2f us B %.2f us | max chunk B %.2f us, max item %.2f us\n", pr[4], pr[5],
+                pr[0] / 100.0 / (pr[4] ? pr[4] : 1), pr[3] / 100.0 / (pr[4] ? pr[4] : 1),
+                pr[1] / 100.0 / (pr[5] ? pr[5] : 1), pr[2] / 100.0 / (pr[5] ? pr[5] : 1), pr[6] / 100.0,
+                pr[7] / 100.0);
+        memset(pr, 0, sizeof(pr));
+        hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), pr, sizeof(pr));
+        static std::vector<unsigned long long> it(1 << 18);
+        hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_item_dur), it.size() * 8);
+        uint64_t hist[8] = {0}, hsum[8] = {0};           // by duration: <25, <50, <100, <200, <400, <800, <1600, more us
+        unsigned long long top = 0;
+        size_t top_i = 0;
+        for (size_t i = 0; i < it.size(); ++i) {
+            const double us = (it[i] >> 24) / 100.0;
+            if (!it[i]) continue;
+            int b = us < 25 ? 0 : us < 50 ? 1 : us < 100 ? 2 : us < 200 ? 3 : us < 400 ? 4 : us < 800 ? 5 : us < 1600 ? 6 : 7;
+            hist[b]++;
+            hsum[b] += (it[i] >> 8) & 0xFFFF;
+            if (it[i] > top) { top = it[i]; top_i = i; }
+        }
+        fprintf(stderr, "[rprof] items by duration <25/50/100/200/400/800/1600/more us: ");
+        for (int b = 0; b < 8; ++b) fprintf(stderr, "%llu(%.1f ch) ", (unsigned long long)hist[b], hist[b] ? (double)hsum[b] / hist[b] : 0.0);
+        fprintf(stderr, "| slowest item %zu: %.1f us, %llu chunks, flags %llu\n", top_i, (top >> 24) / 100.0,
+                (top >> 8) & 0xFFFF, top & 3);
+        std::fill(it.begin(), it.end(), 0ull);
+        hipMemcpyToSymbol(HIP_SYMBOL(g_item_dur), it.data(), it.size() * 8);
+}
+#endif
+
 // Sorted path (sorted_path.inc) for the whole batch: k_resolve (stop point), then per
-// window of kWindow changesets a level-1 (+ level-2) stable partition of the applied
-// records and the per-bucket LDS resolve.  offs = host offsets of the batch, whose
-// device copy c->d_offs was uploaded by phase_scan for this same batch.
-int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wall, const long long* d_event,
-                 crdt_result* out, size_t ev_base) {
+// window of kWindow changesets a level-1 (+ level-2) partition of the applied records and
+// the per-bucket LDS resolve.  sg = the batch's changeset segments (host), in changeset
+// order; one changeset may be several segments (records routed in from several ranks).
+int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
+                 crdt_result* out) {
     const uint32_t R = c->plan_R;
     if (!c->resolved)
         k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     c->resolved = false;
-    ev_record(c, ev_base);
+    ev_record(c, kEvApply);
     c->windows.clear();
     c->apply_total = 1;
-    if (c->timing) { c->windows.push_back({0u, 1u}); ev_record(c, ev_base + 1); }
+    if (c->timing) ev_record(c, ev_window(0, false));
     const bool two = c->cap > (1ull << 20);
     const uint32_t shift1 = two ? 20u : (uint32_t)kSBits;
-    for (uint32_t jb = 0; jb < R; jb += kWindow) {
-        const uint32_t je = std::min<uint32_t>(R, jb + kWindow);
-        const uint32_t nseg = je - jb;
-        const uint64_t nw = offs[je] - offs[jb];
+    const size_t ns_all = sg.j.size();
+    for (size_t sb = 0; sb < ns_all;) {
+        const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
+        size_t se = sb;
+        uint64_t nw = 0;
+        while (se < ns_all && sg.j[se] < jb + kWindow) { nw += sg.end[se] - sg.beg[se]; ++se; }
+        const uint32_t nseg = (uint32_t)(se - sb);
+        const size_t s0 = sb;
+        sb = se;
         if (nw == 0) continue;
-        // host plan: level-1 tile prefix over the window's changesets + the one-segment scan map
+        // host plan: segment bounds and changesets, level-1 tile prefix, the one-segment scan map
         // (the pinned staging buffer is reused: the previous window's copy must have run)
-        if (jb > 0) HIPCHK(hipStreamSynchronize(c->stream));
-        const size_t tb_words = (nseg + 2) / 2;
-        HIPALLOC(c->h_pplan.ensure(tb_words + 3));
-        HIPALLOC(c->p_plan.ensure(tb_words + 3));
-        uint32_t* tb = reinterpret_cast<uint32_t*>(c->h_pplan.p);
+        if (s0 > 0) HIPCHK(hipStreamSynchronize(c->stream));
+        const size_t u32_words = (2 * (size_t)nseg + 2) / 2;        // seg_j [nseg] + tb [nseg + 1]
+        const size_t words = 2 * (size_t)nseg + u32_words + 3;
+        HIPALLOC(c->h_pplan.ensure(words));
+        HIPALLOC(c->p_plan.ensure(words));
+        uint64_t* h_beg = c->h_pplan.p;
+        uint64_t* h_end = c->h_pplan.p + nseg;
+        uint32_t* h_sj = reinterpret_cast<uint32_t*>(c->h_pplan.p + 2 * (size_t)nseg);
+        uint32_t* tb = h_sj + nseg;
         uint32_t nt1 = 0;
         for (uint32_t s = 0; s <= nseg; ++s) {
             tb[s] = nt1;
-            if (s < nseg) nt1 += (uint32_t)((offs[jb + s + 1] - offs[jb + s] + kPTile - 1) / kPTile);
+            if (s < nseg) {
+                h_beg[s] = sg.beg[s0 + s];
+                h_end[s] = sg.end[s0 + s];
+                h_sj[s] = sg.j[s0 + s];
+                nt1 += (uint32_t)((h_end[s] - h_beg[s] + kPTile - 1) / kPTile);
+            }
         }
         const uint32_t nc1 = (nt1 + kChunkTiles - 1) / kChunkTiles;
-        uint32_t* sm_t = reinterpret_cast<uint32_t*>(c->h_pplan.p + tb_words);
+        const size_t tail = 2 * (size_t)nseg + u32_words;
+        uint32_t* sm_t = reinterpret_cast<uint32_t*>(c->h_pplan.p + tail);
         sm_t[0] = 0; sm_t[1] = nt1;                                   // scan tbase {0, nt1}
-        uint32_t* sm_c = reinterpret_cast<uint32_t*>(c->h_pplan.p + tb_words + 1);
+        uint32_t* sm_c = reinterpret_cast<uint32_t*>(c->h_pplan.p + tail + 1);
         sm_c[0] = 0; sm_c[1] = nc1;                                   // scan cbase {0, nc1}
-        c->h_pplan.p[tb_words + 2] = 0;                               // seg_pos {0}
-        HIPCHK(hipMemcpyAsync(c->p_plan.p, c->h_pplan.p, (tb_words + 3) * sizeof(uint64_t), hipMemcpyHostToDevice,
+        c->h_pplan.p[tail + 2] = 0;                                   // seg_pos {0}
+        HIPCHK(hipMemcpyAsync(c->p_plan.p, c->h_pplan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice,
                               c->stream));
         const uint32_t nt2 = two ? (uint32_t)((nw + kPTile - 1) / kPTile) + kDigits : 0;
         const uint32_t nc2 = two ? (nt2 + kChunkTiles - 1) / kChunkTiles + kDigits : 0;
@@ -1305,12 +1473,15 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         HIPALLOC(c->p_choff.ensure((size_t)ncm * kDigits));
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
         HIPALLOC(c->p1_rec.ensure(nw)); HIPALLOC(c->p1_kj.ensure(nw));
-        const uint32_t* d_tb1 = reinterpret_cast<const uint32_t*>(c->p_plan.p);
+        const uint64_t* d_beg = c->p_plan.p;
+        const uint64_t* d_end = c->p_plan.p + nseg;
+        const uint32_t* d_sj = reinterpret_cast<const uint32_t*>(c->p_plan.p + 2 * (size_t)nseg);
+        const uint32_t* d_tb1 = d_sj + nseg;
         HIPALLOC(c->p_tseg.ensure(ntm));
         k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1, c->p_tseg.p);
-        const TileMap tm1{c->d_offs + jb, d_tb1, c->p_tseg.p, nseg};
-        const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words),
-                          reinterpret_cast<const uint32_t*>(c->p_plan.p + tb_words + 1), c->p_plan.p + tb_words + 2, 1};
+        const TileMap tm1{d_beg, d_end, d_tb1, c->p_tseg.p, d_sj, nseg};
+        const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tail),
+                          reinterpret_cast<const uint32_t*>(c->p_plan.p + tail + 1), c->p_plan.p + tail + 2, 1};
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
         k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1, c->p_hist.p);
         k_scan_part<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, sm1, c->p_part.p);
@@ -1329,10 +1500,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
             k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2);
             k_seg_index<<<std::min<uint32_t>(grid_for(nt2, 256), 4096), 256, 0, c->stream>>>(tb2, kDigits, nt2,
                                                                                             c->p_tseg.p);
-            const TileMap tm2{c->p_l1beg.p, tb2, c->p_tseg.p, kDigits};
+            const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(
-                c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
+            k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
                                                                   c->p_hist.p);
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
@@ -1383,133 +1553,83 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const uint64_t* offs, int64_t wa
         }
         HIPCHK(hipGetLastError());
     }
-    if (c->timing) ev_record(c, ev_base + 2);
-    HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-#ifdef CRDT_PROF_RESOLVE
-    {
-        unsigned long long pr[8];
-        hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprof), sizeof(pr));
-        fprintf(stderr, "[rprof] items %llu chunks %llu | per item: init %.2f us final %.2f us | per chunk: "
-                "A %.2f us B %.2f us | max chunk B %.2f us, max item %.2f us\n", pr[4], pr[5],
-                pr[0] / 100.0 / (pr[4] ? pr[4] : 1), pr[3] / 100.0 / (pr[4] ? pr[4] : 1),
-                pr[1] / 100.0 / (pr[5] ? pr[5] : 1), pr[2] / 100.0 / (pr[5] ? pr[5] : 1), pr[6] / 100.0,
-                pr[7] / 100.0);
-        memset(pr, 0, sizeof(pr));
-        hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), pr, sizeof(pr));
-        static std::vector<unsigned long long> it(1 << 18);
-        hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_item_dur), it.size() * 8);
-        uint64_t hist[8] = {0}, hsum[8] = {0};           // by duration: <25, <50, <100, <200, <400, <800, <1600, more us
-        unsigned long long top = 0;
-        size_t top_i = 0;
-        for (size_t i = 0; i < it.size(); ++i) {
-            const double us = (it[i] >> 24) / 100.0;
-            if (!it[i]) continue;
-            int b = us < 25 ? 0 : us < 50 ? 1 : us < 100 ? 2 : us < 200 ? 3 : us < 400 ? 4 : us < 800 ? 5 : us < 1600 ? 6 : 7;
-            hist[b]++;
-            hsum[b] += (it[i] >> 8) & 0xFFFF;
-            if (it[i] > top) { top = it[i]; top_i = i; }
-        }
-        fprintf(stderr, "[rprof] items by duration <25/50/100/200/400/800/1600/more us: ");
-        for (int b = 0; b < 8; ++b) fprintf(stderr, "%llu(%.1f ch) ", (unsigned long long)hist[b], hist[b] ? (double)hsum[b] / hist[b] : 0.0);
-        fprintf(stderr, "| slowest item %zu: %.1f us, %llu chunks, flags %llu\n", top_i, (top >> 24) / 100.0,
-                (top >> 8) & 0xFFFF, top & 3);
-        std::fill(it.begin(), it.end(), 0ull);
-        hipMemcpyToSymbol(HIP_SYMBOL(g_item_dur), it.data(), it.size() * 8);
+    if (c->timing) {
+        ev_record(c, ev_window(0, true));
+        c->windows.push_back(1u);
     }
+    HIPCHK(hipGetLastError());
+#ifdef CRDT_PROF_RESOLVE
+    HIPCHK(hipStreamSynchronize(c->stream));
+    prof_resolve_report();
 #endif
-    crdt_result res = c->h_misc->result;
-    c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
-    uint64_t np = 0, nw_ = 0;
-    for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw_ += c->h_misc->won[s]; }
-    res.n_present = c->counts ? np : UINT64_MAX;       // the order-free form does not count them
-    res.n_won = c->counts ? nw_ : UINT64_MAX;
-    if (c->h_misc->err) res.status = CRDT_E_KEY_RANGE;
-    c->canonical = res.canonical_lt;
-    if (out) *out = res;
-    return res.status;
+    return finish_apply(c, nullptr, nullptr, 0, true, out);
 }
 
 // The sorted path runs for crdt_merge when its preconditions hold (sorted_path.inc
 // header) and either CRDT_MERGE_PATH=sorted or the batch is a multi-changeset fan-in
-// large enough to amortise the partition passes.
-bool use_sorted(const crdt_ctx* c, const crdt_batch* b, const uint8_t* win_flags) {
+// large enough to amortise the partition passes.  R = changesets of the call.
+bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* win_flags) {
     if (c->merge_path == 1 || win_flags || c->canonical < 0 || c->cap > kSortedMaxCap) return false;
-    const uint32_t R = b->n_changesets;
-    for (uint32_t jb = 0; jb < R; jb += kWindow) {
-        const uint32_t je = std::min<uint32_t>(R, jb + kWindow);
-        if (b->offsets[je] - b->offsets[jb] >= (1ull << 31)) return false;
+    uint64_t n = 0, nw = 0;
+    uint32_t jb = 0;
+    for (size_t s = 0; s < sg.j.size(); ++s) {              // < 2^31 records per kWindow changesets
+        if (sg.j[s] >= jb + kWindow) { jb = sg.j[s] - sg.j[s] % kWindow; nw = 0; }
+        nw += sg.end[s] - sg.beg[s];
+        n += sg.end[s] - sg.beg[s];
+        if (nw >= (1ull << 31)) return false;
     }
     if (c->merge_path == 2) return true;
     // auto: many small changesets (cfg3-like fan-in), where one partitioned pass beats R
     // latency-bound K2 launches; large changesets keep K2 (measured)
-    const uint64_t n = b->offsets[R];
     return R >= 64 && n >= (8ull << 20) && n / R <= (256ull << 10);
 }
 
+// Apply phase over columns whose changeset segments are c->segs (n = column length).
+int apply_segs(crdt_ctx* c, const Cols& cols, uint64_t n, int32_t mem, int64_t wall, const long long* d_event,
+               uint8_t* win_flags, crdt_result* out, bool allow_sorted) {
+    if (c->timing) HIPCHK(ensure_events(c, events_for(c->segs.j.size())));
+    c->last_sorted = allow_sorted && use_sorted(c, c->segs, c->plan_R, win_flags);
+    if (c->last_sorted) {
+        int st = kv_copy_all(c);
+        if (st) return st;
+        return apply_sorted(c, cols, c->segs, wall, d_event, out);
+    }
+    return apply_ranges(c, cols, c->segs, n, mem, wall, d_event, win_flags, out);
+}
+
 int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long long* d_event,
-                uint8_t* win_flags, crdt_result* out, size_t ev_base, bool allow_sorted = false) {
+                uint8_t* win_flags, crdt_result* out, bool allow_sorted = false) {
     int st = validate_batch(owned);
     if (st) return st;
     const uint32_t R = c->plan_R;
     if (owned->n_changesets != R) return CRDT_E_INVALID;
     Cols cols;
     if ((st = stage_apply_cols(c, owned, &cols))) return st;
-    c->last_sorted = allow_sorted && use_sorted(c, owned, win_flags);
-    if (c->last_sorted) {
-        if ((st = kv_copy_all(c))) return st;
-        return apply_sorted(c, cols, owned->offsets, wall, d_event, out, ev_base);
-    }
-    return apply_ranges(c, cols, owned->offsets, owned->offsets + 1, owned->offsets[R], owned->mem, wall, d_event,
-                        win_flags, out, ev_base);
+    c->segs.from_offsets(owned->offsets, R);
+    return apply_segs(c, cols, owned->offsets[R], owned->mem, wall, d_event, win_flags, out, allow_sorted);
 }
 
-// Upload a batch's offsets + tile starts into the routing plan (kept apart from the merge plan).
-int upload_route_plan(crdt_ctx* c, const crdt_batch* b, uint32_t* max_tiles) {
-    const uint32_t R = b->n_changesets;
-    const size_t words = (R + 1) + (R + 2) / 2;
-    HIPALLOC(c->h_rplan.ensure(words));
-    HIPALLOC(c->d_rplan.ensure(words));
-    uint64_t* h_offs = c->h_rplan.p;
-    uint32_t* h_tstart = reinterpret_cast<uint32_t*>(c->h_rplan.p + (R + 1));
-    uint64_t tiles = 0;
-    uint32_t mt = 0;
-    for (uint32_t j = 0; j <= R; ++j) {
-        h_offs[j] = b->offsets[j];
-        h_tstart[j] = (uint32_t)tiles;
-        if (j < R) {
-            const uint64_t tj = (b->offsets[j + 1] - b->offsets[j] + kTile - 1) / kTile;
-            tiles += tj;
-            mt = std::max<uint32_t>(mt, (uint32_t)tj);
-        }
-    }
-    if (tiles >= (1ull << 32)) return CRDT_E_INVALID;
-    HIPCHK(hipMemcpyAsync(c->d_rplan.p, c->h_rplan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-    *max_tiles = mt;
-    return CRDT_OK;
-}
-
-void collect_timing(crdt_ctx* c, uint32_t R, bool full) {
+void collect_timing(crdt_ctx* c) {
     crdt_timing t{};
-    if (c->timing && full) {
+    if (c->timing) {
         float ms = 0;
-        // events: 0 start, 1 after scan, 2 after clock/verify/resolve, 3 = apply base, then pairs
-        if (hipEventElapsedTime(&ms, c->events[0], c->events[1]) == hipSuccess) t.scan_ms = ms;
-        if (hipEventElapsedTime(&ms, c->events[1], c->events[2]) == hipSuccess) t.clock_ms = ms;
-        for (const auto& w : c->windows) {
-            const size_t a = 4 + 2 * (size_t)w.first, b = a + 1;
-            float d = 0;
-            if (hipEventElapsedTime(&d, c->events[a], c->events[b]) == hipSuccess) {
-                t.apply_ms += d;
-                t.apply_launches += w.second;
-            }
+        auto el = [&](size_t a, size_t b) {
+            return hipEventElapsedTime(&ms, c->events[a], c->events[b]) == hipSuccess ? (double)ms : 0.0;
+        };
+        t.scan_ms = el(kEvStart, kEvScan);
+        t.clock_ms = el(kEvScan, kEvClock);
+        t.route_ms = el(kEvClock, kEvApply);
+        for (size_t k = 0; k < c->windows.size(); ++k) {
+            t.apply_ms += el(ev_window(k, false), ev_window(k, true));
+            t.apply_launches += c->windows[k];
         }
         t.apply_total = c->apply_total;
-        const size_t last = 3 + 2 * (size_t)R + 1;
-        if (hipEventElapsedTime(&ms, c->events[0], c->events[last]) == hipSuccess) t.total_ms = ms;
+        t.total_ms = el(kEvStart, kEvEnd);
     }
     c->last_timing = t;
 }
+
+#include "comm_path.inc"
 
 }  // namespace
 
@@ -1529,6 +1649,7 @@ const char* crdt_status_string(int s) {
         case CRDT_E_NOMEM: return "device out of memory";
         case CRDT_E_KEY_RANGE: return "key id out of range";
         case CRDT_E_NO_DEVICE: return "no gfx950 device";
+        case CRDT_E_COMM: return "communicator error";
         default: return "unknown status";
     }
 }
@@ -1584,6 +1705,11 @@ void crdt_destroy(crdt_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    comm_release(c);
+    for (auto* b : {&c->r_skey, &c->r_srank, &c->r_sval, &c->r_key, &c->r_rank, &c->r_val}) b->release();
+    c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
+    c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release();
+    c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
     if (c->table) hipFree(c->table);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
@@ -1596,7 +1722,6 @@ void crdt_destroy(crdt_ctx* c) {
     c->s_millis.release(); c->s_mod.release(); c->s_flags.release(); c->s_out.release();
     c->d_word.release();
     c->d_ibase.release();
-    c->h_ibase.release();
     c->p1_rec.release(); c->p1_kj.release(); c->p2_rec.release(); c->p2_kj.release();
     c->p_hist.release(); c->p_toff.release(); c->p_part.release(); c->p_choff.release();
     c->p_dstart1.release(); c->p_dstart2.release(); c->p_l2map.release();
@@ -1829,6 +1954,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         return CRDT_OK;
     }
     HIPCHK(hipSetDevice(c->device));
+    if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
     // Host batches are staged once; every phase then sees device columns.
     crdt_batch dev = *batch;
     uint8_t* dflags = win_flags;
@@ -1860,157 +1986,22 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         }
     }
     HIPALLOC(c->d_M.ensure(R));
-    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
-    ev_record(c, 0);
+    if (c->timing) HIPCHK(ensure_events(c, events_for(R)));
+    ev_record(c, kEvStart);
     if ((st = phase_scan(c, &dev, wall, c->d_M.p, true))) return st;
-    ev_record(c, 1);
+    ev_record(c, kEvScan);
     if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
     if (!c->resolved && (st = phase_resolve(c, c->d_event.p))) return st;
-    ev_record(c, 2);
-    st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, 3, true);
+    ev_record(c, kEvClock);
+    st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, true);
     if (c->timing) {
-        ev_record(c, 3 + 2 * (size_t)R + 1);
+        ev_record(c, kEvEnd);
         hipStreamSynchronize(c->stream);
     }
     if (st >= 0 && win_flags && batch->mem == CRDT_MEM_HOST && n)
         HIPCHK(hipMemcpy(win_flags, dflags, n, hipMemcpyDeviceToHost));
-    collect_timing(c, R, true);
+    collect_timing(c);
     return st;
-}
-
-int crdt_merge_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, uint64_t* d_maxima) {
-    if (!c || !d_maxima) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    if (c->timing && home) HIPCHK(ensure_events(c, 4 + 2 * (size_t)home->n_changesets + 1));
-    ev_record(c, 0);
-    int st = phase_scan(c, home, wall, reinterpret_cast<long long*>(d_maxima));
-    if (st) return st;
-    ev_record(c, 1);
-    HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_maxima next
-    return CRDT_OK;
-}
-
-int crdt_merge_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const uint64_t* d_maxima,
-                     const int64_t* d_prefix_max, const uint64_t* index_base, uint64_t* d_event) {
-    if (!c || !d_maxima || !d_event) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    int st = phase_clock(c, home, wall, reinterpret_cast<const long long*>(d_maxima),
-                         reinterpret_cast<long long*>(d_event), reinterpret_cast<const long long*>(d_prefix_max),
-                         index_base);
-    if (st) return st;
-    HIPCHK(hipStreamSynchronize(c->stream));    // the host all-reduces d_event[0] next
-    return CRDT_OK;
-}
-
-int crdt_merge_resolve(crdt_ctx* c, const crdt_batch* home, uint64_t* d_event) {
-    if (!c || !d_event || !home || home->n_changesets != c->plan_R) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    int st = phase_resolve(c, reinterpret_cast<long long*>(d_event));
-    if (st) return st;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return CRDT_OK;
-}
-
-int crdt_merge_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const uint64_t* d_event,
-                     uint8_t* win_flags, crdt_result* out) {
-    if (!c || !d_event) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    // timing (when enabled): scan_ms = the scan call, clock_ms = scan end -> apply start (clock, verify,
-    // resolve and the host collectives between the calls), apply launches sampled as in crdt_merge
-    const uint32_t R = c->plan_R;
-    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
-    ev_record(c, 2);
-    int st = phase_apply(c, owned, wall, reinterpret_cast<const long long*>(d_event), win_flags, out, 3);
-    if (c->timing) {
-        ev_record(c, 3 + 2 * (size_t)R + 1);
-        hipStreamSynchronize(c->stream);
-    }
-    collect_timing(c, R, true);
-    return st;
-}
-
-int crdt_merge_apply_segments(crdt_ctx* c, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
-                              const uint32_t* val, uint64_t n, const uint64_t* seg_begin, const uint64_t* seg_end,
-                              int64_t wall, const uint64_t* d_event, uint8_t* win_flags, crdt_result* out) {
-    if (!c || !d_event) return CRDT_E_INVALID;
-    const uint32_t R = c->plan_R;
-    if (R && (!seg_begin || !seg_end)) return CRDT_E_INVALID;
-    for (uint32_t j = 0; j < R; ++j)
-        if (seg_begin[j] > seg_end[j] || seg_end[j] > n) return CRDT_E_INVALID;
-    if (n && (!key_id || !lt || !rank || !val)) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    Cols cols;
-    cols.key = key_id; cols.lt = lt; cols.rank = rank; cols.val = val;
-    if (c->timing) HIPCHK(ensure_events(c, 4 + 2 * (size_t)R + 1));
-    ev_record(c, 2);
-    int st = apply_ranges(c, cols, seg_begin, seg_end, n, CRDT_MEM_DEVICE, wall,
-                          reinterpret_cast<const long long*>(d_event), win_flags, out, 3);
-    if (c->timing) {
-        ev_record(c, 3 + 2 * (size_t)R + 1);
-        hipStreamSynchronize(c->stream);
-    }
-    collect_timing(c, R, true);
-    return st;
-}
-
-int crdt_route_count(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, uint64_t* counts) {
-    if (!c || !counts || n_ranks == 0 || n_ranks > (uint32_t)kRouteMaxRanks) return CRDT_E_INVALID;
-    int st = validate_batch(batch);
-    if (st) return st;
-    const uint32_t R = batch->n_changesets;
-    const uint64_t n = batch->offsets[R];
-    if (n && !batch->key_id) return CRDT_E_INVALID;
-    const size_t cells = (size_t)R * n_ranks;
-    if (!cells) return CRDT_OK;
-    HIPCHK(hipSetDevice(c->device));
-    const uint32_t* key;
-    if ((st = stage(c, c->s_key, batch->key_id, n, batch->mem, &key))) return st;
-    uint32_t mt = 0;
-    if ((st = upload_route_plan(c, batch, &mt))) return st;
-    HIPALLOC(c->d_rcount.ensure(cells));
-    HIPCHK(hipMemsetAsync(c->d_rcount.p, 0, cells * sizeof(unsigned long long), c->stream));
-    const uint64_t* offs = c->d_rplan.p;
-    const uint32_t* tstart = reinterpret_cast<const uint32_t*>(c->d_rplan.p + (R + 1));
-    if (mt) {
-        const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, std::max<uint32_t>(1, 65536u / R)));
-        for (uint32_t jb = 0; jb < R; jb += 65535)
-            k_route_count<<<dim3(gx, std::min<uint32_t>(65535, R - jb)), kScanThreads, 0, c->stream>>>(
-                key, offs, tstart, jb, n_ranks, c->d_rcount.p);
-        HIPCHK(hipGetLastError());
-    }
-    HIPCHK(hipMemcpyAsync(counts, c->d_rcount.p, cells * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return CRDT_OK;
-}
-
-int crdt_route_scatter(crdt_ctx* c, const crdt_batch* batch, uint32_t n_ranks, const uint64_t* send_base,
-                       uint32_t* out_slot, int64_t* out_lt, uint32_t* out_rank, uint32_t* out_val,
-                       uint64_t* out_perm) {
-    if (!c || n_ranks == 0 || n_ranks > (uint32_t)kRouteMaxRanks) return CRDT_E_INVALID;
-    int st = validate_batch(batch);
-    if (st) return st;
-    const uint32_t R = batch->n_changesets;
-    const uint64_t n = batch->offsets[R];
-    if (!n) return CRDT_OK;
-    if (!send_base || !out_slot || !out_lt || !out_rank || !out_val) return CRDT_E_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    Cols cols;
-    if ((st = stage_apply_cols(c, batch, &cols))) return st;
-    uint32_t mt = 0;
-    if ((st = upload_route_plan(c, batch, &mt))) return st;
-    const size_t cells = (size_t)R * n_ranks;
-    HIPALLOC(c->d_rcount.ensure(cells));
-    HIPCHK(hipMemcpyAsync(c->d_rcount.p, send_base, cells * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-    const uint64_t* offs = c->d_rplan.p;
-    const uint32_t* tstart = reinterpret_cast<const uint32_t*>(c->d_rplan.p + (R + 1));
-    const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, std::max<uint32_t>(1, 65536u / R)));
-    for (uint32_t jb = 0; jb < R; jb += 65535)
-        k_route_scatter<<<dim3(gx, std::min<uint32_t>(65535, R - jb)), kScanThreads, 0, c->stream>>>(
-            cols.key, cols.lt, cols.rank, cols.val, offs, tstart, jb, n_ranks, c->d_rcount.p, out_slot, out_lt,
-            out_rank, out_val, out_perm);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return CRDT_OK;
 }
 
 int crdt_set_counts(crdt_ctx* c, int exact) {

@@ -26,12 +26,27 @@ def _is_torch(a) -> bool:
 
 
 _NP_TYPES = {"u4": np.uint32, "i8": np.int64, "u1": np.uint8}
+# torch dtypes a device column of each kind may have (same element width; the kernels
+# reinterpret the bits, so int32 carries uint32 ids / handles)
+_TORCH_KINDS = {"u4": ("int32", "uint32"), "i8": ("int64",), "u1": ("uint8", "bool")}
+
+
+def check_device_tensor(t, kind: str, device: int, name: str = "tensor"):
+    """A GPU tensor handed to the library by pointer: contiguous, of the kind's element width
+    and on the ctx's device (the kernels index it by element; a wrong width reads past its end)."""
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    dt = str(t.dtype).replace("torch.", "")
+    if dt not in _TORCH_KINDS[kind]:
+        raise ValueError(f"{name}: dtype {dt} where {'/'.join(_TORCH_KINDS[kind])} is expected")
+    if t.device.index is not None and device is not None and t.device.index != device:
+        raise ValueError(f"{name} is on cuda:{t.device.index}, the table on cuda:{device}")
 
 
 class _Cols:
     """Normalises a set of columns to one memory kind and keeps them alive."""
 
-    def __init__(self, **cols):
+    def __init__(self, device=None, **cols):
         self.keep = []
         self.mem = None
         self.ptrs = {}
@@ -43,8 +58,7 @@ class _Cols:
                 if not arr.is_cuda:
                     arr = arr.numpy()
                 else:
-                    if not arr.is_contiguous():
-                        raise ValueError(f"column {name} must be contiguous")
+                    check_device_tensor(arr, kind, device, f"column {name}")
                     mem = _capi.CRDT_MEM_DEVICE
                     self._set_mem(mem)
                     self.keep.append(arr)
@@ -88,6 +102,11 @@ class DeviceTable:
         except Exception:
             pass
 
+    def _dptr(self, t, kind: str, name: str):
+        """Device pointer of a GPU tensor argument after the width / device checks."""
+        check_device_tensor(t, kind, self.device, name)
+        return ctypes.c_void_p(t.data_ptr())
+
     def _check(self, st: int, what: str):
         if st < 0:
             raise CrdtNativeError(st, what)
@@ -125,7 +144,7 @@ class DeviceTable:
 
     # ---------------------------------------------------------------------- SPI
     def put_rows(self, key, lt, rank, val, mod):
-        c = _Cols(key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), mod=(mod, "i8"))
+        c = _Cols(self.device, key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), mod=(mod, "i8"))
         n = len(key)
         p = c.ptrs
         self._check(self._lib.crdt_put_rows(self._ctx, p["key"], p["lt"], p["rank"], p["val"], p["mod"],
@@ -168,14 +187,14 @@ class DeviceTable:
 
     # ---------------------------------------------------------------- Crdt API
     def put_stamped(self, key, val, wall: int) -> dict:
-        c = _Cols(key=(key, "u4"), val=(val, "u4"))
+        c = _Cols(self.device, key=(key, "u4"), val=(val, "u4"))
         res = CrdtResult()
         self._check(self._lib.crdt_put_stamped(self._ctx, c.ptrs["key"], c.ptrs["val"], len(key), int(wall),
                                                c.mem, ctypes.byref(res)), "crdt_put_stamped")
         return res.as_dict()
 
     def _batch(self, key, lt, rank, val, offsets, millis):
-        c = _Cols(key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), millis=(millis, "i8"))
+        c = _Cols(self.device, key=(key, "u4"), lt=(lt, "i8"), rank=(rank, "u4"), val=(val, "u4"), millis=(millis, "i8"))
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         c.keep.append(offs)
         b = CrdtBatch(c.ptrs["key"], c.ptrs["lt"], c.ptrs["rank"], c.ptrs["val"], c.ptrs["millis"],
@@ -201,75 +220,50 @@ class DeviceTable:
                 fptr = flags_arr.ctypes.data_as(ctypes.c_void_p)
         elif win_flags is not None and win_flags is not False:
             flags_arr = win_flags
-            fptr = ctypes.c_void_p(win_flags.data_ptr()) if _is_torch(win_flags) else \
-                win_flags.ctypes.data_as(ctypes.c_void_p)
+            if _is_torch(win_flags):
+                fptr = self._dptr(win_flags, "u1", "win_flags")
+            else:
+                if win_flags.dtype != np.uint8 or not win_flags.flags.c_contiguous or len(win_flags) < n:
+                    raise ValueError("win_flags must be a contiguous uint8 array of one entry per record")
+                fptr = win_flags.ctypes.data_as(ctypes.c_void_p)
         res = CrdtResult()
-        self._check(self._lib.crdt_merge(self._ctx, ctypes.byref(b), int(wall), fptr, ctypes.byref(res)),
-                    "crdt_merge")
+        st = self._lib.crdt_merge(self._ctx, ctypes.byref(b), int(wall), fptr, ctypes.byref(res))
+        if st == _capi.CRDT_E_COMM and getattr(self, "_comm", None) is not None and self._comm.error is not None:
+            raise CrdtNativeError(st, f"crdt_merge (communicator: {self._comm.error!r})")
+        self._check(st, "crdt_merge")
         if flags_arr is not None and win_flags is True:
             flags_arr = flags_arr[:n]
         return res.as_dict(), flags_arr
 
-    # ----------------------------------------------- key-sharded phases (RCCL)
-    def merge_scan(self, home, wall: int, d_maxima):
-        b, c, _ = self._batch(*home)
-        self._check(self._lib.crdt_merge_scan(self._ctx, ctypes.byref(b), int(wall),
-                                              ctypes.c_void_p(d_maxima.data_ptr())), "crdt_merge_scan")
+    # ------------------------------------------ key-sharded replica (comm_path.inc)
+    def comm_unique_id(self) -> bytes:
+        """crdt_comm_unique_id: the 128 bytes rank 0 hands every rank (RCCL)."""
+        buf = (ctypes.c_uint8 * _capi.COMM_ID_BYTES)()
+        self._check(self._lib.crdt_comm_unique_id(buf), "crdt_comm_unique_id")
+        return bytes(buf)
 
-    def merge_clock(self, home, wall: int, d_maxima, d_event, d_prefix_max=None, index_base=None):
-        b, c, _ = self._batch(*home)
-        ib = None if index_base is None else np.ascontiguousarray(index_base, dtype=np.uint64)
-        self._check(self._lib.crdt_merge_clock(
-            self._ctx, ctypes.byref(b), int(wall), ctypes.c_void_p(d_maxima.data_ptr()),
-            None if d_prefix_max is None else ctypes.c_void_p(d_prefix_max.data_ptr()),
-            None if ib is None else ib.ctypes.data_as(ctypes.c_void_p),
-            ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_clock")
+    def comm_init_rccl(self, n_ranks: int, rank: int, uid: bytes):
+        buf = (ctypes.c_uint8 * _capi.COMM_ID_BYTES).from_buffer_copy(uid)
+        self._check(self._lib.crdt_comm_init_rccl(self._ctx, n_ranks, rank, buf), "crdt_comm_init_rccl")
 
-    def merge_resolve(self, home, d_event):
-        b, c, _ = self._batch(*home)
-        self._check(self._lib.crdt_merge_resolve(self._ctx, ctypes.byref(b),
-                                                 ctypes.c_void_p(d_event.data_ptr())), "crdt_merge_resolve")
+    def comm_init_ops(self, n_ranks: int, rank: int, comm):
+        """Join a communicator given as a crdt_comm_ops table (``comm.ops()``, e.g. dist.GlooComm)."""
+        self._comm = comm                      # the callbacks must outlive the ctx's use of them
+        ops = comm.ops()
+        st = self._lib.crdt_comm_init_ops(self._ctx, n_ranks, rank, ctypes.byref(ops))
+        self._check(st, "crdt_comm_init_ops")
 
-    def merge_apply(self, owned, wall: int, d_event, win_flags=None):
-        b, c, _ = self._batch(*owned)
-        fptr = None if win_flags is None else ctypes.c_void_p(win_flags.data_ptr())
-        res = CrdtResult()
-        self._check(self._lib.crdt_merge_apply(self._ctx, ctypes.byref(b), int(wall),
-                                               ctypes.c_void_p(d_event.data_ptr()), fptr, ctypes.byref(res)),
-                    "crdt_merge_apply")
-        return res.as_dict()
+    def comm_info(self) -> tuple[int, int]:
+        n, r = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.crdt_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(r)), "crdt_comm_info")
+        return n.value, r.value
 
-    # ---------------------------------------------- routed multi-GPU (all-to-all)
-    def route_count(self, batch, n_ranks: int) -> np.ndarray:
-        """[R, n_ranks] uint64: records of changeset j owned by rank d (key % n_ranks)."""
-        b, c, offs = self._batch(*batch)
-        R = len(offs) - 1
-        out = np.zeros((R, n_ranks), np.uint64)
-        self._check(self._lib.crdt_route_count(self._ctx, ctypes.byref(b), n_ranks,
-                                               out.ctypes.data_as(ctypes.c_void_p)), "crdt_route_count")
-        return out
+    def comm_free(self):
+        self._check(self._lib.crdt_comm_free(self._ctx), "crdt_comm_free")
 
-    def route_scatter(self, batch, n_ranks: int, send_base, out_slot, out_lt, out_rank, out_val, out_perm=None):
-        """Partition ``batch`` into the device send columns; chunk (j, d) starts at send_base[j, d]."""
-        b, c, _ = self._batch(*batch)
-        base = np.ascontiguousarray(send_base, dtype=np.uint64)
-        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        self._check(self._lib.crdt_route_scatter(
-            self._ctx, ctypes.byref(b), n_ranks, base.ctypes.data_as(ctypes.c_void_p), P(out_slot), P(out_lt),
-            P(out_rank), P(out_val), None if out_perm is None else P(out_perm)), "crdt_route_scatter")
-
-    def merge_apply_segments(self, cols, seg_begin, seg_end, wall: int, d_event, win_flags=None) -> dict:
-        """Apply phase over device columns (key_slot, lt, rank, val); changeset j = [seg_begin[j], seg_end[j])."""
-        key, lt, rank, val = cols
-        sb = np.ascontiguousarray(seg_begin, dtype=np.uint64)
-        se = np.ascontiguousarray(seg_end, dtype=np.uint64)
-        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        res = CrdtResult()
-        self._check(self._lib.crdt_merge_apply_segments(
-            self._ctx, P(key), P(lt), P(rank), P(val), int(key.numel()), sb.ctypes.data_as(ctypes.c_void_p),
-            se.ctypes.data_as(ctypes.c_void_p), int(wall), P(d_event),
-            None if win_flags is None else P(win_flags), ctypes.byref(res)), "crdt_merge_apply_segments")
-        return res.as_dict()
+    def set_presharded(self, on: bool):
+        """True: batches hold only records this rank owns, with key = slot (no record exchange)."""
+        self._check(self._lib.crdt_set_presharded(self._ctx, 1 if on else 0), "crdt_set_presharded")
 
     # ---------------------------------------------------------------- timing
     PATHS = {"auto": 0, "gather": 1, "sorted": 2}

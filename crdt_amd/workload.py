@@ -54,9 +54,11 @@ def _zipf_keys(n: int, rows: int, K: int, s: float, gen: torch.Generator, device
 def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_local: int = 1 << 27,
               s: float = 0.8, seed: int = 0xC0FFEE04, device="cuda", order: str = "shuffled",
               rank: int = 0, world: int = 1, chunk: int = 64, millis_span: int = 1 << 16,
-              counter_span: int = 16, route: bool = False) -> dict:
+              counter_span: int = 16, route: bool = False, census: bool = False) -> dict:
     """``route``: records are NOT pre-split by owner — this rank keeps the full changesets it is
-    home to (``home`` gets key and val too, ``owned`` is empty) for the routed protocol."""
+    home to (``home`` gets key and val too, ``owned`` is empty) for the routed protocol.
+    ``census``: also count U_touch of SURVEY §8(d) for this rank's slots — the distinct keys of
+    the whole batch that it owns and that are present in the local map (``u_touch``)."""
     dev = torch.device(device)
     n = -(-total // R)                                   # records per replica (ceil)
     wall = BASE_MILLIS + millis_span + 1000
@@ -66,9 +68,14 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
     own_counts = np.zeros(R, np.int64)
     home = {"lt": [], "rank": []}
     home_counts = np.zeros(R, np.int64)
+    seen = torch.zeros(-(-K // world), dtype=torch.bool, device=dev) if census else None
     for j0 in range(0, R, chunk):
         rows = min(chunk, R - j0)
         key = _zipf_keys(n, rows, K, s, gen, dev)
+        if census:
+            kk = key[(key % world) == rank] if world > 1 else key.reshape(-1)
+            seen[kk // world] = True
+            del kk
         if order == "shuffled":
             perm = torch.argsort(torch.rand(rows, n, device=dev, generator=gen), dim=1)
             key = torch.gather(key, 1, perm)
@@ -125,6 +132,8 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
     l_rank = torch.randint(0, R + 1, (n_local,), device=dev, generator=lgen)
     l_lt_all = (l_ms << 16) + l_cnt
     c0 = int(l_lt_all.max().item())                    # refreshCanonicalTime() of the full replica
+    u_touch = int(seen[:nl].sum().item()) if census else None
+    del seen
     local = {"slot": (lids // world).to(torch.int32), "lt": l_lt_all[lids].contiguous(),
              "rank": l_rank[lids].to(torch.int32), "val": (lids & 0x7FFFFFFF).to(torch.int32),
              "mod": l_lt_all[lids].contiguous()}
@@ -136,6 +145,7 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
         "home_offsets": np.concatenate([[0], np.cumsum(home_counts)]).astype(np.uint64),
         "local": local, "n_local_rows": nl, "capacity": slots_total, "c0": c0, "wall": wall,
         "R": R, "n_per_replica": n, "total": n * R, "K": K, "n_local": n_local, "world": world, "rank": rank,
+        "u_touch": u_touch,
     }
 
 

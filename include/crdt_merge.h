@@ -22,8 +22,11 @@
  * negative mod.
  *
  * Domain: |millis| < 2^47 for every clock and wall value (Dart int wraps past it).
- * Threading: a ctx is one replica (one GPU); calls on one ctx are synchronous and
- * must not run concurrently, exactly like the single-isolate reference.
+ * Threading: a ctx is one replica shard (one GPU); calls on one ctx are synchronous and
+ * must not run concurrently, exactly like the single-isolate reference.  A ctx joined
+ * to a communicator (crdt_comm_init_*) is one of n_ranks key shards of ONE replica: its
+ * crdt_merge calls are collective (every rank calls with the same n_changesets and
+ * wall_millis) and the library runs the exchanges itself (SURVEY §8(b) "Threading").
  */
 #ifndef CRDT_MERGE_H
 #define CRDT_MERGE_H
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CRDT_ABI_VERSION 1
+#define CRDT_ABI_VERSION 2
 #define CRDT_NULL_VALUE 0xFFFFFFFFu
 
 /* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
@@ -48,7 +51,8 @@ enum crdt_status {
     CRDT_E_HIP = -2,           /* HIP runtime error */
     CRDT_E_NOMEM = -3,         /* device allocation failed */
     CRDT_E_KEY_RANGE = -4,     /* a key_id >= capacity: state after the call is unspecified */
-    CRDT_E_NO_DEVICE = -5      /* no usable gfx950 device */
+    CRDT_E_NO_DEVICE = -5,     /* no usable gfx950 device */
+    CRDT_E_COMM = -6           /* the communicator failed (RCCL error, missing librccl, a callback's error) */
 };
 
 /* Where the column pointers of a call live. */
@@ -90,12 +94,14 @@ typedef struct crdt_result {
  * ctx stream (bench / roofline support; zeros unless enabled). */
 typedef struct crdt_timing {
     double scan_ms;            /* K3a: per-changeset max + candidate tiles */
-    double clock_ms;           /* K3b/K3c: canonical prefix-max scan, exception resolution */
+    double clock_ms;           /* K3b/K3c: canonical prefix-max scan, exception resolution (+ the
+                                  clock collectives on a sharded ctx) */
     double apply_ms;           /* K2: summed durations of SAMPLED windows of back-to-back apply launches
                                   (8 launches every 32; the sorted path: its whole apply region) */
     uint32_t apply_launches;   /* apply launches inside the sampled windows */
     uint32_t apply_total;      /* apply launches in the call */
     double total_ms;           /* first to last event of the call */
+    double route_ms;           /* sharded ctx: route count, count exchange, scatter, record exchange */
 } crdt_timing;
 
 /* ---- lifecycle ------------------------------------------------------------ */
@@ -154,53 +160,64 @@ int crdt_refresh_canonical(crdt_ctx* ctx, uint64_t n_rows, int64_t* out_lt);
 int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint8_t* win_flags,
                crdt_result* out);
 
-/* ---- key-sharded multi-GPU phases ------------------------------------------
- * crdt_merge() == scan -> clock -> resolve -> apply on one ctx.  With keys
- * sharded over G ranks, each rank scans the changesets it is home to (a batch
- * with all R changesets, non-home ones empty), and between phases the host
- * all-reduces the device words (RCCL over xGMI); all are plain signed int64:
- *   d_maxima [R] : MAX all-reduce after scan   (M_j = max lt of changeset j; INT64_MIN: empty)
- *   d_event  [4] : MIN all-reduce of d_event[0] after clock (first exception, (j << 40) | i;
- *                  INT64_MAX: none), then MAX all-reduce of d_event[1..3] after resolve
- *                  (canonical at the failure, kind, Hlc.millis of the failing record)
- * then applies the records it owns (any rank: owned batch, same n_changesets).
- * scan and clock synchronise the ctx stream before returning.
+/* ---- key-sharded multi-GPU (north star config 4) -------------
+ * n_ranks ctxs — one per GPU, normally one process per GPU — form ONE replica whose
+ * keys are sharded: rank d owns key k iff k % n_ranks == d and stores it at slot
+ * k / n_ranks (so each ctx's capacity counts slots).  crdt_merge on such a ctx is
+ * collective: every rank passes the same n_changesets and wall_millis and its own
+ * PART of each changeset; changeset j is the concatenation, in rank order, of the
+ * ranks' parts (a Map's iteration order is whatever its sender produced, so this is a
+ * legal order; a replica that arrives whole on one rank is the case where the other
+ * parts are empty).  Inside the call the library:
+ *   1. scans its parts (per-part max, tiles that may raise);
+ *   2. all-gathers the R part maxima and counts -> M_j, and each part's preceding
+ *      max / record offset inside changeset j;
+ *   3. runs the canonical recurrence and exception scan, MIN all-reduce of the first
+ *      event, MAX all-reduce of its details -> the same stop point everywhere;
+ *   4. counts its records per (owner, changeset), exchanges the counts, scatters the
+ *      records into owner-major send columns {slot, lt, rank, val} and moves them with
+ *      ONE grouped all-to-all (every column of every peer in one group);
+ *   5. applies the records it received (gather or sorted path) with mod = R_j;
+ *   6. SUM all-reduce of the per-record counts and of the key-range error.
+ * Every rank returns the same status, stop point, canonical and counts; win_flags
+ * (optional, [n] of the local batch) come back to the rank that passed the record.
+ * Keys in the batch are GLOBAL key ids, unless crdt_set_presharded(ctx, 1): then every
+ * record is already on its owner and key_id holds its slot (no record exchange).
  *
- * "Parts" protocol (changeset j = the concatenation, in rank order, of the parts
- * the ranks own): every rank scans its own part; the host all-gathers the R maxima,
- * passes the global max in d_maxima, the max of the lower ranks' parts in
- * d_prefix_max (device, [R]) and their record counts in index_base (host, [R]).
- * The home protocol passes NULL for both. */
-int crdt_merge_scan(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis, uint64_t* d_maxima);
-int crdt_merge_clock(crdt_ctx* ctx, const crdt_batch* home, int64_t wall_millis,
-                     const uint64_t* d_maxima, const int64_t* d_prefix_max, const uint64_t* index_base,
-                     uint64_t* d_event);
-int crdt_merge_resolve(crdt_ctx* ctx, const crdt_batch* home, uint64_t* d_event);
-int crdt_merge_apply(crdt_ctx* ctx, const crdt_batch* owned, int64_t wall_millis,
-                     const uint64_t* d_event, uint8_t* win_flags, crdt_result* out);
+ * Backends: RCCL over xGMI (crdt_comm_unique_id on one rank, the host broadcasts the
+ * 128 bytes, crdt_comm_init_rccl on every rank; librccl is opened on first use), or a
+ * caller's crdt_comm_ops table (a host transport: MPI, TCP, gloo).  No reference
+ * counterpart: the reference is single-process (example/crdt_example.dart:21-25). */
+enum crdt_reduce_op { CRDT_REDUCE_SUM = 0, CRDT_REDUCE_MAX = 1, CRDT_REDUCE_MIN = 2 };
 
-/* ---- routed multi-GPU (records arrive on their changeset's home rank) -------
- * North star config 4 / SURVEY §8(e) step 5: the home rank partitions its batch by
- * owner rank d = key_id % n_ranks (slot key_id / n_ranks), the host exchanges the
- * chunks with RCCL all-to-all, and each owner applies changeset j from wherever its
- * records landed.  No reference counterpart (the reference is single-process).
- *
- * crdt_route_count: counts[j * n_ranks + d] = records of changeset j owned by d (HOST out).
- * crdt_route_scatter: writes the batch's records into the send columns (DEVICE), chunk
- *   (j, d) starting at send_base[j * n_ranks + d] (HOST in); order inside a chunk is
- *   unspecified; out_perm (optional) receives each sent record's index in the batch.
- * crdt_merge_apply_segments: the apply phase over DEVICE columns of length n where
- *   changeset j is rows [seg_begin[j], seg_end[j]) (HOST arrays of the plan's R);
- *   win_flags (optional, DEVICE [n]) indexed like the columns.  Same result as
- *   crdt_merge_apply. */
-int crdt_route_count(crdt_ctx* ctx, const crdt_batch* batch, uint32_t n_ranks, uint64_t* counts);
-int crdt_route_scatter(crdt_ctx* ctx, const crdt_batch* batch, uint32_t n_ranks, const uint64_t* send_base,
-                       uint32_t* out_slot, int64_t* out_lt, uint32_t* out_rank, uint32_t* out_val,
-                       uint64_t* out_perm);
-int crdt_merge_apply_segments(crdt_ctx* ctx, const uint32_t* key_id, const int64_t* lt, const uint32_t* rank,
-                              const uint32_t* val, uint64_t n, const uint64_t* seg_begin,
-                              const uint64_t* seg_end, int64_t wall_millis, const uint64_t* d_event,
-                              uint8_t* win_flags, crdt_result* out);
+typedef struct crdt_comm_ops {
+    void* user;                /* passed back to every callback */
+    int32_t mem;               /* CRDT_MEM_DEVICE: pointers are device memory and an operation is
+                                  ordered on `stream` (a hipStream_t) like RCCL's;
+                                  CRDT_MEM_HOST: the library synchronises, stages the words through
+                                  host memory and the call completes before it returns */
+    int32_t reserved;
+    /* in-place all-reduce of n signed 64-bit words */
+    int (*all_reduce_i64)(void* user, int64_t* words, uint64_t n, int32_t op, void* stream);
+    /* recv[r * n + i] = send[i] of rank r */
+    int (*all_gather_i64)(void* user, const int64_t* send, int64_t* recv, uint64_t n, void* stream);
+    /* one grouped exchange of n_cols columns (column c has elem_bytes[c]-byte elements): to each
+       peer d this rank sends elements [send_displs[d], + send_counts[d]) of every column and
+       receives [recv_displs[d], + recv_counts[d]) from it; the entries for this rank are 0 (the
+       library moves its own chunk itself) */
+    int (*all_to_all_v)(void* user, uint32_t n_cols, const void* const* send_cols, void* const* recv_cols,
+                        const uint32_t* elem_bytes, const uint64_t* send_counts, const uint64_t* send_displs,
+                        const uint64_t* recv_counts, const uint64_t* recv_displs, void* stream);
+} crdt_comm_ops;
+
+#define CRDT_COMM_ID_BYTES 128
+int crdt_comm_unique_id(uint8_t* id /* [CRDT_COMM_ID_BYTES] */);
+int crdt_comm_init_rccl(crdt_ctx* ctx, uint32_t n_ranks, uint32_t rank, const uint8_t* id);
+int crdt_comm_init_ops(crdt_ctx* ctx, uint32_t n_ranks, uint32_t rank, const crdt_comm_ops* ops);
+int crdt_comm_info(const crdt_ctx* ctx, uint32_t* n_ranks, uint32_t* rank);
+int crdt_comm_free(crdt_ctx* ctx);
+/* presharded = 1: batches hold only records this rank owns, key_id = slot (no exchange) */
+int crdt_set_presharded(crdt_ctx* ctx, int presharded);
 
 /* ---- merge strategy --------------------------------------------------------
  * crdt_merge resolves a batch either by the gather path (one launch per changeset,

@@ -23,6 +23,9 @@
  * faithful != 0 additionally mirrors the reference's cost structure: one full
  * snapshot copy of the local map per merge (map_crdt.dart:43) and one wall
  * clock read per remote record (hlc.dart:82).  Results do not depend on it.
+ * faithful = T > 1 runs the snapshot copy on T threads (the bulk map copy is the
+ * only part of the reference algorithm with no order; the recv loop and the
+ * winner loop stay sequential, as in the reference).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -97,9 +100,12 @@ int or_merge(or_row* table, uint64_t cap, int64_t* canonical, uint32_t local_ran
         uint64_t b = offsets[j], e = offsets[j + 1];
         const or_row* local = table;
         if (faithful) {                                  /* recordMap(): copy + filter */
-            memcpy(snap, table, cap * sizeof(or_row));
-            for (uint64_t k = 0; k < cap; ++k)
+            const int64_t ncap = (int64_t)cap;
+#pragma omp parallel for schedule(static) num_threads(faithful) if (faithful > 1)
+            for (int64_t k = 0; k < ncap; ++k) {
+                snap[k] = table[k];
                 if (snap[k].mod < 0) snap[k].mod = INT64_MIN;
+            }
             local = snap;
         }
         /* removeWhere: recv loop over every record (may throw, map untouched) */

@@ -34,32 +34,38 @@ def test_bench_line_contract(gpu_device, path):
     for k in KEYS:
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
-    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["data"] == "synthetic"
+    assert d["higher_is_better"] is True and d["scaling"] == "strong" and d["data"] == "synthetic"
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["config"]["records"] == 4000000 and d["config"]["merge_path"] == path
-    rf = d["roofline"]
+    rf, job = d["roofline"], d["job"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # the contract fraction: SURVEY 8(d)'s B_alg over distinct keys / step time
+    b_alg = 20 * d["config"]["records"] + 12 * job["U_touch"] + 24 * job["U_win"]
+    assert job["B_alg_bytes"] == b_alg
+    assert abs(rf["frac"] - b_alg / (d["ms_per_step"] / 1e3) / 8e12) < 2e-3
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert d["parity"]["equal"] is True and d["parity"]["fields_differing"] == 0
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_weak(gpu_device):
-    """The N > 1 bench path (parts protocol, weak scaling) with 2 ranks on one GPU over gloo:
-    the driver's N = 2..8 runs take the same code with RCCL, one GPU per rank."""
+def test_bench_two_ranks_routed(gpu_device):
+    """The N > 1 bench path (config 4: the same records in total, replica j on rank j % N, routed
+    to key % N inside the library's collective merge) with 2 ranks on one GPU over the gloo
+    communicator: the driver's N = 2..8 runs take the same code with RCCL, one GPU per rank."""
     env = dict(os.environ, CRDT_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--records", "4000000", "--replicas", "16"]
     # (default key space: torch.distributed.run's own parser takes `--local` for `--local-addr`)
-    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]                  # rank 0 prints the one line
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    assert d["config"]["parallelism"] == "keyshard2-parts"
-    assert d["config"]["records"] == 2 * 4000000                  # weak: every rank its own part
-    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == "keyshard2-routed" and d["config"]["records"] == 4000000
+    assert d["value"] == pytest.approx(4000000 / (d["ms_per_step"] / 1e3), rel=1e-3)
+    assert d["presharded"]["value"] > 0
+    assert d["job"]["U_touch"] > 0 and d["job"]["U_win"] > 0

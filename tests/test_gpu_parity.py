@@ -207,27 +207,31 @@ def test_reserve_preserves_rows(gpu_device):
 
 def _init_pg(dist, rank, world, backend):
     import torch
-    if backend == "nccl":                      # RCCL: the collectives the bench runs at N > 1
+    if backend == "nccl":                      # the bench's process group at N > 1
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
     else:
         dist.init_process_group(backend, rank=rank, world_size=world)
 
 
-def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home", backend="gloo"):
+def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path="gather", counts=True):
+    """One rank of a sharded replica on cuda:0: the library's collective crdt_merge
+    (comm_path.inc) over RCCL (backend nccl) or the host-staged gloo communicator."""
     import os
 
     import torch
     import torch.distributed as dist
 
     from crdt_amd import DeviceTable
-    from crdt_amd.dist import route_by_owner, sharded_merge, sharded_merge_parts, torch_all_gather, torch_reducers
-    from tests.test_dist_cpu import _parts_case, _split
+    from crdt_amd.dist import GlooComm, attach_rccl
+    from tests.test_dist_cpu import layout
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     _init_pg(dist, rank, world, backend)
     try:
-        case = make_case(**case_kw) if protocol == "home" else _parts_case(case_kw, world)
+        case, sel, part_offs = layout(make_case(**case_kw), world, rank, kind)
         cap = -(-case["n_ids"] // world)
         t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
+        t.set_merge_path(path)
+        t.set_counts(counts)
         loc = case["local"]
         ids = np.arange(case["n_local"])
         mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
@@ -235,217 +239,166 @@ def _sharded_gpu_worker(rank, world, port, case_kw, q, protocol="home", backend=
             t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
                        loc["val"][mine], loc["mod"][mine])
         t.canonical = case["c0"]
-        owned, home, idx = _split(case, world, rank)
-        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-        owned_d = (dev(owned[0]), dev(owned[1]), dev(owned[2]), dev(owned[3]), owned[4], None)
-        home_d = (None, dev(home[1]), dev(home[2]), None, home[4], dev(home[5]))
-        R = len(case["offsets"]) - 1
-        d_max = torch.zeros(max(R, 1), dtype=torch.int64, device="cuda")
-        d_ev = torch.zeros(4, dtype=torch.int64, device="cuda")
-        flags = torch.zeros(max(len(idx), 1), dtype=torch.uint8, device="cuda")
-        red_max, red_min = torch_reducers(dist)
-        if protocol == "home":
-            res = sharded_merge(t, home_d, owned_d, case["wall"], d_max, d_ev, red_max, red_min, win_flags=flags)
+        if backend == "nccl":
+            attach_rccl(t, dist)
         else:
-            routes = route_by_owner(case["key"], case["offsets"], world)
-            counts = np.stack([np.diff(routes[r][1].astype(np.int64)) for r in range(world)])
-            ibase = counts[:rank].sum(axis=0)
-            part = owned_d[:5] + (None if case["millis"] is None else dev(case["millis"][idx]),)
-            res = sharded_merge_parts(t, part, case["wall"], ibase, d_max, d_ev, torch_all_gather(dist), red_max,
-                                      red_min, rank, win_flags=flags)
+            t.comm_init_ops(world, rank, GlooComm(dist))
+        assert t.comm_info() == (world, rank)
+        t.set_presharded(kind == "presharded")
+        key = case["key"][sel]
+        if kind == "presharded":
+            key = key // world
+        dev = lambda a: None if a is None else torch.from_numpy(  # noqa: E731
+            np.ascontiguousarray(a.view(np.int32) if a.dtype == np.uint32 else a)).cuda()
+        millis = None if case["millis"] is None else dev(case["millis"][sel])
+        flags = torch.zeros(max(len(sel), 1), dtype=torch.uint8, device="cuda") if path == "gather" else False
+        res, _ = t.merge(dev(key.astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]),
+                         dev(case["val"][sel]), part_offs, case["wall"], millis=millis, win_flags=flags)
+        res["path"] = t.last_path()
         lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
-        q.put((rank, res, lt, rk, val, mod, idx, flags[:len(idx)].cpu().numpy()))
+        fl = flags[:len(sel)].cpu().numpy() if path == "gather" else None
+        q.put((rank, res, lt, rk, val, mod, sel, fl))
         t.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("protocol", ["home", "parts"])
-@pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
-def test_two_rank_sharded_on_device(gpu_device, name, protocol):
-    """The device phase API under the multi-rank protocols (2 processes on one GPU, gloo)."""
+def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True):
     import torch.multiprocessing as mp
 
-    from tests.test_dist_cpu import _free_port, _parts_case
-    kw = dict(CASE_SPECS)[name]
-    case = make_case(**kw) if protocol == "home" else _parts_case(kw, 2)
+    from tests.test_dist_cpu import _free_port, layout
+    case, _, _ = layout(make_case(**kw), world, 0, kind)
     orows, ores, oflags = oracle_run(case)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_gpu_worker, args=(r, 2, port, kw, q, protocol)) for r in range(2)]
+    procs = [ctx.Process(target=_shard_gpu_worker, args=(r, world, port, kw, kind, q, backend, path, counts))
+             for r in range(world)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=180) for _ in range(2)]
+    outs = sorted([q.get(timeout=180) for _ in range(world)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     flags = np.zeros(len(case["key"]), np.uint8)
-    tot = [0, 0]
-    for rank, res, lt, rk, val, mod, idx, fl in outs:
-        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
-            assert res[f] == ores[f], (name, rank, f)
-        tot[0] += res["n_present"]
-        tot[1] += res["n_won"]
-        flags[idx] = fl
+    for rank, res, lt, rk, val, mod, sel, fl in outs:
+        for f in RESULT_FIELDS:
+            if f in ("n_present", "n_won") and not counts and res["path"] == "sorted":
+                assert res[f] == (1 << 64) - 1
+                continue
+            assert res[f] == ores[f], (kind, rank, f, res[f], ores[f])
+        if fl is not None:
+            flags[sel] = fl
         keys = np.arange(case["n_ids"])
-        mine = keys % 2 == rank
-        slots = keys[mine] // 2
+        mine = keys % world == rank
+        slots = keys[mine] // world
         for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
-            assert np.array_equal(a[slots], orows[f][mine]), f
-    assert tot == [ores["n_present"], ores["n_won"]]
-    assert np.array_equal(flags, oflags)
+            assert np.array_equal(a[slots], orows[f][mine]), (kind, f)
+    if path == "gather":
+        assert np.array_equal(flags, oflags)
+    return outs
 
 
-def _routed_gpu_worker(rank, world, port, case_kw, q, backend="gloo"):
+@pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
+@pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
+def test_two_rank_sharded_on_device(gpu_device, name, kind):
+    """The library's collective crdt_merge, 2 ranks on one GPU over the gloo communicator:
+    every row of both shards, win flags, canonical, exception fields, counts vs the oracle."""
+    run_shard_gpu(dict(CASE_SPECS)[name], 2, kind)
+
+
+@pytest.mark.parametrize("counts", [True, False])
+def test_two_rank_routed_sorted_path(gpu_device, counts):
+    """Routed records resolved by the sorted path: changeset j is one segment per source rank
+    (tile map with segment ends and changesets); 300 tie-heavy changesets, 3 ranks."""
+    kw = dict(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8, counter_span=4,
+              n_ranks=301)
+    outs = run_shard_gpu(kw, 3, "parts", path="sorted", counts=counts)
+    assert all(o[1]["path"] == "sorted" for o in outs)
+
+
+@pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
+@pytest.mark.parametrize("name", ["r8_tombstones", "drift_late"])
+def test_rccl_single_rank(gpu_device, name, kind):
+    """The same call over RCCL (crdt_comm_init_rccl, one rank): the device-side all-gather /
+    all-reduce and the grouped exchange path the bench takes at N > 1."""
+    run_shard_gpu(dict(CASE_SPECS)[name], 1, kind, backend="nccl")
+
+
+def test_rccl_single_rank_sorted(gpu_device):
+    kw = dict(seed=80, R=200, per_cs=3000, n_local=30_000, n_new=30_000, millis_span=8, counter_span=4,
+              n_ranks=201, tomb_frac=0.1)
+    outs = run_shard_gpu(kw, 1, "routed", backend="nccl", path="sorted", counts=False)
+    assert outs[0][1]["path"] == "sorted"
+
+
+def _fanin_shard_worker(rank, world, port, q, K, total, R):
+    """Routed fan-in (gen_fanin's home layout) on one rank; returns this shard's rows."""
     import os
 
     import torch
     import torch.distributed as dist
 
     from crdt_amd import DeviceTable
-    from crdt_amd.dist import sharded_merge_routed, torch_all_gather, torch_all_to_all, torch_alloc, torch_reducers
-    from tests.test_dist_cpu import _home_batch
+    from crdt_amd.dist import GlooComm
+    from crdt_amd.workload import gen_fanin
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    _init_pg(dist, rank, world, backend)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        case = make_case(**case_kw)
-        cap = -(-case["n_ids"] // world)
-        t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
-        loc = case["local"]
-        ids = np.arange(case["n_local"])
-        mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
-        if mine.any():
-            t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
-                       loc["val"][mine], loc["mod"][mine])
-        t.canonical = case["c0"]
-        home, sel = _home_batch(case, world, rank)
-        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-        home_d = (dev(home[0]), dev(home[1]), dev(home[2]), dev(home[3]), home[4], dev(home[5]))
-        R = len(case["offsets"]) - 1
-        d_max = torch.zeros(max(R, 1), dtype=torch.int64, device="cuda")
-        d_ev = torch.zeros(4, dtype=torch.int64, device="cuda")
-        flags = torch.zeros(len(sel), dtype=torch.uint8, device="cuda")
-        red_max, red_min = torch_reducers(dist)
-        res = sharded_merge_routed(t, home_d, case["wall"], d_max, d_ev, red_max, red_min, torch_all_gather(dist),
-                                   torch_all_to_all(dist), rank, world, torch_alloc("cuda"), win_flags=flags)
-        lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
-        q.put((rank, res, lt, rk, val, mod, sel, flags.cpu().numpy()))
+        wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda", rank=rank, world=world,
+                       route=True)
+        t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+        t.set_counts(False)
+        t.set_merge_path("sorted")
+        loc, home = wl["local"], wl["home"]
+        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        t.canonical = wl["c0"]
+        t.comm_init_ops(world, rank, GlooComm(dist))
+        res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
+                         win_flags=False)
+        q.put((rank, res, t.last_path(), t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))))
         t.close()
+        torch.cuda.empty_cache()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
-def test_two_rank_routed_on_device(gpu_device, name):
-    """Routed protocol on device: k_route_count / k_route_scatter, all-to-all, segmented K2."""
+def test_two_rank_routed_fanin_equals_one_gpu(gpu_device):
+    """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
+    routed to key % 2) give exactly the rows and canonical of the unsharded merge."""
     import torch.multiprocessing as mp
 
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
     from tests.test_dist_cpu import _free_port
-    kw = dict(CASE_SPECS)[name]
-    case = make_case(**kw)
-    orows, ores, oflags = oracle_run(case)
+    K, total, R = 1 << 22, 4_000_000, 128
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+    t.set_merge_path("gather")                                # the reference: K2, unsharded
+    loc, own = wl["local"], wl["owned"]
+    t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+    t.canonical = wl["c0"]
+    ref, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                     win_flags=False)
+    rows = t.read_rows(np.arange(K, dtype=np.uint32))
+    t.close()
+    del wl
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_routed_gpu_worker, args=(r, 2, port, kw, q)) for r in range(2)]
+    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R)) for r in range(2)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=180) for _ in range(2)]
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    flags = np.zeros(len(case["key"]), np.uint8)
-    tot = [0, 0]
-    for rank, res, lt, rk, val, mod, sel, fl in outs:
-        for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter"):
-            assert res[f] == ores[f], (name, rank, f)
-        tot[0] += res["n_present"]
-        tot[1] += res["n_won"]
-        flags[sel] = fl
-        keys = np.arange(case["n_ids"])
-        mine = keys % 2 == rank
-        slots = keys[mine] // 2
-        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
-            assert np.array_equal(a[slots], orows[f][mine]), f
-    assert tot == [ores["n_present"], ores["n_won"]]
-    assert np.array_equal(flags, oflags)
-
-
-@pytest.mark.parametrize("protocol", ["home", "parts", "routed"])
-@pytest.mark.parametrize("name", ["r8_tombstones", "drift_late"])
-def test_rccl_single_rank_protocols(gpu_device, name, protocol):
-    """The three multi-GPU protocols over RCCL (backend ``nccl``) with one rank: the device-side
-    all-reduce / all-gather / all-to-all branches of crdt_amd/dist.py that the bench takes at N > 1
-    (the gloo tests above stage through the host)."""
-    import torch.multiprocessing as mp
-
-    from tests.test_dist_cpu import _free_port
-    kw = dict(CASE_SPECS)[name]
-    case = make_case(**kw)
-    orows, ores, oflags = oracle_run(case)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    if protocol == "routed":
-        p = ctx.Process(target=_routed_gpu_worker, args=(0, 1, port, kw, q, "nccl"))
-    else:
-        p = ctx.Process(target=_sharded_gpu_worker, args=(0, 1, port, kw, q, protocol, "nccl"))
-    p.start()
-    rank, res, lt, rk, val, mod, sel, fl = q.get(timeout=180)
-    p.join(timeout=60)
-    assert p.exitcode == 0
-    for f in ("status", "n_stored", "exc_changeset", "exc_index", "canonical_lt", "drift_ms", "counter",
-              "n_present", "n_won"):
-        assert res[f] == ores[f], (name, protocol, f)
-    flags = np.zeros(len(case["key"]), np.uint8)
-    flags[sel] = fl
-    assert np.array_equal(flags, oflags)
-    for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
-        assert np.array_equal(a, orows[f]), f
-
-
-def test_route_kernels_partition(gpu_device):
-    """k_route_count / k_route_scatter on a 3M-record, 5-changeset batch for 8 owners: counts,
-    chunk contents (as multisets) and perm against numpy."""
-    import torch
-
-    from crdt_amd import DeviceTable
-    rng = np.random.default_rng(3)
-    R, G = 5, 8
-    sizes = [700_001, 0, 1_200_000, 4097, 1_095_902]
-    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
-    n = int(offs[-1])
-    key = rng.integers(0, 1 << 30, n, dtype=np.uint32)
-    lt = rng.integers(0, 1 << 60, n, dtype=np.int64)
-    rank = rng.integers(0, 1000, n, dtype=np.uint32)
-    val = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-    t = DeviceTable(0, capacity=16)
-    d = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).cuda()  # noqa: E731
-    batch = (d(key), d(lt), d(rank), d(val), offs, None)
-    counts = t.route_count(batch, G)
-    exp = np.zeros((R, G), np.uint64)
-    for j in range(R):
-        exp[j] = np.bincount(key[offs[j]:offs[j + 1]] % G, minlength=G)
-    assert np.array_equal(counts, exp)
-    ca = counts.astype(np.int64)[None]                       # a single holder: rank 0 of a 1-rank view
-    sb = (np.concatenate([[0], np.cumsum(ca[0].sum(axis=0))[:-1]])[None, :] + np.cumsum(ca[0], axis=0) - ca[0])
-    outs = [torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int64, device="cuda"),
-            torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda")]
-    perm = torch.empty(n, dtype=torch.int64, device="cuda")
-    t.route_scatter(batch, G, sb.astype(np.uint64), *outs, out_perm=perm)
-    slot, olt, ork, ov = (o.cpu().numpy() for o in outs)
-    p = perm.cpu().numpy()
-    assert np.array_equal(np.sort(p), np.arange(n))          # a permutation
-    assert np.array_equal(slot.view(np.uint32), key[p] // G)
-    assert np.array_equal(olt, lt[p]) and np.array_equal(ork.view(np.uint32), rank[p])
-    assert np.array_equal(ov.view(np.uint32), val[p])
-    for j in range(R):                                       # chunk (j, d) holds exactly its records
-        for g in range(G):
-            a, c = int(sb[j, g]), int(counts[j, g])
-            seg = p[a:a + c]
-            assert np.all((seg >= offs[j]) & (seg < offs[j + 1])) and np.all(key[seg] % G == g)
-    t.close()
+    for rank, res, path, shard in outs:
+        assert path == "sorted"
+        for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
+            assert res[f] == ref[f], (rank, f)
+        for a, b in zip(shard, rows):
+            assert np.array_equal(a, b[rank::2]), rank
 
 
 # ------------------------------------------------------------------ sorted path
