@@ -103,10 +103,16 @@ struct Misc {
     uint32_t tiles_hot;    // scan tiles holding a record above C_0, every kHotSample-th (next scan's form)
     uint32_t pad;
     crdt_result result;    // filled by k_resolve
+    // frame of the batch's records (k_scan<*, *, true>) for the sorted path's packed key
+    // (sorted_path.inc), as max-accumulators whose identity is the memset's 0:
+    //   fr_lo = max(~ord(lt)), fr_hi = max(ord(lt)), ord(x) = x ^ 2^63 (int64 order as uint64);
+    //   fr_rlo = max(~rank), fr_rhi = max(rank)
+    unsigned long long fr_lo, fr_hi;
+    uint32_t fr_rlo, fr_rhi;
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
-    unsigned long long pad16;  // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
-};                             // kernel (1112 B took an aligned fill plus a tail fill, ~5 us each)
+};                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
+                               // kernel (1112 B took an aligned fill plus a tail fill, ~5 us each)
 static_assert(sizeof(Misc) % 16 == 0, "Misc is memset as whole 16-B words");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -144,7 +150,12 @@ constexpr uint32_t kHotSample = 16;              // tiles_hot counts every 16th 
 // deltas); otherwise only waves holding such a record load them (the fan-in: ~none do).
 // kMillis: the batch carries an explicit millis column (an Hlc whose counter exceeds 0xFFFF);
 // without it millis = lt >> 16 and the eager form keeps no millis registers.
-template <bool kEager, bool kMillis = true>
+__host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
+
+// kFrame (the sorted path will run): with rank loaded eagerly, also the frame of the records
+// (lt and rank bounds) into misc->fr_*, one set of atomics per workgroup and tile, only where
+// it moves a bound (a stale read of a bound never makes a needed atomic look useless)
+template <bool kEager, bool kMillis = true, bool kFrame = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
@@ -152,8 +163,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     int64_t wall, uint32_t local_rank,
     int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
 {
+    static_assert(kEager || !kFrame, "the frame needs every rank");
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
+    __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
     const uint32_t j = jbase + blockIdx.y;
     const uint64_t beg = offs[j], end = offs[j + 1];
     const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
@@ -186,11 +199,45 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                 f |= (r == local_rank) | (wsub(ms, wall) > kMaxDrift);
             }
         }
+        unsigned long long flo = 0, fhi = 0, frl = 0, frh = 0;   // max-accumulators (0: none)
+        if (kFrame) {
+#pragma unroll
+            for (int q = 0; q < kScanItems; ++q) {
+                const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+                if (i < end) {
+                    const uint64_t o = ord64(v[q]);
+                    flo = ~o > flo ? ~o : flo;
+                    fhi = o > fhi ? o : fhi;
+                    const uint32_t r = rk[kEager ? q : 0];
+                    frl = (uint32_t)~r > frl ? (uint32_t)~r : frl;
+                    frh = r > frh ? r : frh;
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long a = __shfl_xor(flo, off, 64), b = __shfl_xor(fhi, off, 64);
+                const unsigned long long c = __shfl_xor(frl, off, 64), d = __shfl_xor(frh, off, 64);
+                flo = a > flo ? a : flo; fhi = b > fhi ? b : fhi; frl = c > frl ? c : frl; frh = d > frh ? d : frh;
+            }
+            if (lane == 0) { s_fr[4 * w] = flo; s_fr[4 * w + 1] = fhi; s_fr[4 * w + 2] = frl; s_fr[4 * w + 3] = frh; }
+        }
         m = wave_max(m);
         const int fw = __any(f) | (m > c0 ? 2 : 0);
         if (lane == 0) { s_max[w] = m; s_flag[w] = fw; }
         __syncthreads();
         if (threadIdx.x == 0) {
+            if (kFrame) {
+                for (int k = 1; k < kScanThreads / 64; ++k) {
+                    flo = s_fr[4 * k] > flo ? s_fr[4 * k] : flo;
+                    fhi = s_fr[4 * k + 1] > fhi ? s_fr[4 * k + 1] : fhi;
+                    frl = s_fr[4 * k + 2] > frl ? s_fr[4 * k + 2] : frl;
+                    frh = s_fr[4 * k + 3] > frh ? s_fr[4 * k + 3] : frh;
+                }
+                if (flo > *(volatile unsigned long long*)&misc->fr_lo) atomicMax(&misc->fr_lo, flo);
+                if (fhi > *(volatile unsigned long long*)&misc->fr_hi) atomicMax(&misc->fr_hi, fhi);
+                if ((uint32_t)frl > *(volatile uint32_t*)&misc->fr_rlo) atomicMax(&misc->fr_rlo, (uint32_t)frl);
+                if ((uint32_t)frh > *(volatile uint32_t*)&misc->fr_rhi) atomicMax(&misc->fr_rhi, (uint32_t)frh);
+            }
             int64_t tm = s_max[0];
             int tf = s_flag[0];
             for (int k = 1; k < kScanThreads / 64; ++k) { tm = imax(tm, s_max[k]); tf |= s_flag[k]; }
@@ -673,31 +720,50 @@ __global__ __launch_bounds__(256) void k_flags_back(const uint8_t* __restrict__ 
     if (i < n) flags[perm[i]] = sflags[i];
 }
 
-// Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j.
+// Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j, and
+// gsend[2R .. 2R + 4) = this rank's record frame (Misc::fr_*, max-accumulators).
+constexpr uint32_t kGatherExtra = 4;
 __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict__ offs, uint32_t R,
-                                                     long long* __restrict__ gsend)
+                                                     const Misc* __restrict__ misc, long long* __restrict__ gsend)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j < R) gsend[R + j] = (long long)(offs[j + 1] - offs[j]);
+    if (j == 0) {
+        gsend[2 * R] = (long long)misc->fr_lo;
+        gsend[2 * R + 1] = (long long)misc->fr_hi;
+        gsend[2 * R + 2] = (long long)misc->fr_rlo;
+        gsend[2 * R + 3] = (long long)misc->fr_rhi;
+    }
 }
 
-// From the all-gathered [G][2R] words (part maxima, part counts): M_j over all parts, and
-// for this rank's part the max / record count of the parts before it (lower ranks).
+// From the all-gathered [G][2R + 4] words (part maxima, part counts, frame): M_j over all parts,
+// for this rank's part the max / record count of the parts before it (lower ranks), and the
+// frame of every rank's records (the records this rank will receive lie inside it).
 __global__ __launch_bounds__(256) void k_shard_combine(const long long* __restrict__ g, uint32_t G, uint32_t me,
                                                        uint32_t R, long long* __restrict__ M,
                                                        long long* __restrict__ pbase,
-                                                       unsigned long long* __restrict__ ibase)
+                                                       unsigned long long* __restrict__ ibase,
+                                                       Misc* __restrict__ misc)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t row = 2ull * R + kGatherExtra;
+    if (j == 0) {
+        unsigned long long a = 0, b = 0, c = 0, d = 0;
+        for (uint32_t r = 0; r < G; ++r) {
+            const unsigned long long* w = reinterpret_cast<const unsigned long long*>(g + r * row + 2ull * R);
+            a = w[0] > a ? w[0] : a; b = w[1] > b ? w[1] : b; c = w[2] > c ? w[2] : c; d = w[3] > d ? w[3] : d;
+        }
+        misc->fr_lo = a; misc->fr_hi = b; misc->fr_rlo = (uint32_t)c; misc->fr_rhi = (uint32_t)d;
+    }
     if (j >= R) return;
     int64_t m = INT64_MIN, pm = INT64_MIN;
     uint64_t ib = 0;
     for (uint32_t r = 0; r < G; ++r) {
-        const int64_t v = g[(uint64_t)r * 2 * R + j];
+        const int64_t v = g[(uint64_t)r * row + j];
         m = imax(m, v);
         if (r < me) {
             pm = imax(pm, v);
-            ib += (uint64_t)g[(uint64_t)r * 2 * R + R + j];
+            ib += (uint64_t)g[(uint64_t)r * row + R + j];
         }
     }
     M[j] = m;
@@ -983,6 +1049,10 @@ struct crdt_ctx {
     bool fused = false;             // this plan: tile max in k_clock<true>, resolve in k_verify<true>
     bool scan_eager = false;        // next k_scan loads rank / millis with lt (last call: mostly hot tiles)
     bool no_fuse = false;           // CRDT_NO_FUSE: small merges keep k_tmax / k_resolve_local / k_resolve
+    bool xcd_map = true;            // XCD-contiguous tile order in the partition scatters (CRDT_XCD_MAP=0: off)
+    bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
+    bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
+    bool last_packed = false;       // the last sorted apply used the packed form
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
     Segs segs;                      // changeset segments of the columns the apply phase reads
@@ -1130,7 +1200,10 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 // ---- phases ---------------------------------------------------------------
 // allow_fuse (single-ctx crdt_merge): for small batches the tile-max reduction moves into
 // k_clock<true> and the resolve kernels into the last k_verify<true> workgroup (c->fused).
-int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false) {
+// frame: also reduce the records' lt / rank frame into misc->fr_* (the sorted path's packed key;
+// the scan then reads every rank with its lt).
+int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false,
+               bool frame = false) {
     c->fused = false;
     c->resolved = false;
     int st = validate_batch(home);
@@ -1154,6 +1227,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     c->plan_R = R;
     c->plan_tiles = tiles;
     c->plan_mt = mt;
+    c->frame_on = frame;
     c->fused = allow_fuse && !c->no_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
@@ -1161,7 +1235,15 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (c->scan_eager && !cols.millis)
+            if (frame && !cols.millis)
+                k_scan<true, false, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            else if (frame)
+                k_scan<true, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            else if (c->scan_eager && !cols.millis)
                 k_scan<true, false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
@@ -1425,6 +1507,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     const bool two = c->cap > (1ull << 20);
     const uint32_t shift1 = two ? 20u : (uint32_t)kSBits;
     const size_t ns_all = sg.j.size();
+    // order-free form: packed 12-B payloads and the packed resolve when the scan's frame of the
+    // batch fits the 64-bit key (one read-back of Misc per call), else wide payloads + lists
+    PackFrame pf{};
+    bool pk = false;
+    if (!c->counts && c->packed_resolve && c->frame_on) {
+        HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        pf = make_frame(c->h_misc->fr_lo, c->h_misc->fr_hi, c->h_misc->fr_rlo, c->h_misc->fr_rhi);
+        pk = pf.ok;
+    }
+    c->last_packed = pk;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -1488,9 +1581,15 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
-        k_part_scatter1<<<nt1, kPThreads, 0, c->stream>>>(cols.key, cols.lt, cols.rank, cols.val, tm1, jb,
-                                                           c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                                                           c->p1_kj.p);
+        const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
+        if (pk)
+            k_part_scatter1<true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                c->p1_kj.p, xper1, pf);
+        else
+            k_part_scatter1<false><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                c->p1_kj.p, xper1, pf);
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
@@ -1507,12 +1606,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
             k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
+            // (nt2 is an upper bound of the level-2 tiles; the real count is on the device)
+            const uint32_t xper2 = c->xcd_map ? (nt2 + kXcds - 1) / kXcds : 0;
             if (c->counts)
-                k_part_scatter2<true><<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits,
-                                                                        c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
+                k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+            else if (pk)
+                k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
             else
-                k_part_scatter2<false><<<nt2, kPThreads, 0, c->stream>>>(c->p1_rec.p, c->p1_kj.p, tm2, kSBits,
-                                                                         c->p_toff.p, c->p2_rec.p, c->p2_kj.p);
+                k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
         }
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
         const uint32_t nb = two ? kDigits * kDigits : kDigits;
@@ -1541,7 +1645,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                                     c->cap, ps, cy, c->d_Rj.p, jb);
             k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                      c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
-        } else {        // order-free: no per-record counts; split buckets finished by k_part_carry<true>
+        } else if (pk) {   // packed order-free form: one LDS 64-bit max per record (sorted_path.inc)
+            uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
+            uint32_t* ps_val = c->p_ksu32.p;
+            const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
+            k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf);
+            k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+                d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf);
+            k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
+                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf);
+        } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
                                                                           c->d_misc);
@@ -1679,6 +1793,8 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
         c->merge_path = strcmp(e, "gather") == 0 ? 1 : strcmp(e, "sorted") == 0 ? 2 : 0;
     }
     if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
@@ -1987,8 +2103,11 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     }
     HIPALLOC(c->d_M.ensure(R));
     if (c->timing) HIPCHK(ensure_events(c, events_for(R)));
+    // the sorted path's packed form needs the records' frame: the scan reduces it on the way
+    c->segs.from_offsets(batch->offsets, R);
+    const bool frame = !c->counts && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
     ev_record(c, kEvStart);
-    if ((st = phase_scan(c, &dev, wall, c->d_M.p, true))) return st;
+    if ((st = phase_scan(c, &dev, wall, c->d_M.p, true, frame))) return st;
     ev_record(c, kEvScan);
     if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
     if (!c->resolved && (st = phase_resolve(c, c->d_event.p))) return st;

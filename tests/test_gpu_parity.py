@@ -518,6 +518,70 @@ def test_sorted_large_single_changeset(gpu_device, counts):
     assert res["status"] == 0 and res["path"] == "sorted"
 
 
+def _frame_edge_case(seed):
+    """Local rows placed around the frame of the records (sorted_path.inc, packed resolve): lt
+    just below / at / just above the records' lt range, ranks below / inside / above theirs,
+    equal (lt, rank) with a record — every clamp of pack_local against the list form's rules."""
+    case = make_case(seed=seed, R=40, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=2,
+                     n_ranks=9, local_rank=0, tomb_frac=0.2)
+    rng = np.random.default_rng(seed)
+    lo, hi = int(case["lt"].min()), int(case["lt"].max())
+    rlo, rhi = int(case["rank"].min()), int(case["rank"].max())
+    loc = case["local"]
+    n = case["n_local"]
+    lt_choices = np.array([lo - 1, lo, (lo + hi) // 2, hi, hi + 1], np.int64)
+    loc["lt"] = lt_choices[rng.integers(0, 5, n)]
+    rk_choices = np.array([max(rlo - 1, 0), rlo, (rlo + rhi) // 2, rhi, rhi + 1, 200], np.uint32)
+    loc["rank"] = rk_choices[rng.integers(0, 6, n)]
+    # a tenth of the local rows copy a record of their key exactly (equal (lt, rank): local keeps)
+    first = {}
+    for x, k in enumerate(case["key"].tolist()):
+        first.setdefault(k, x)
+    for k in rng.choice(n, n // 10, replace=False):
+        if int(k) in first:
+            loc["lt"][k] = case["lt"][first[int(k)]]
+            loc["rank"][k] = case["rank"][first[int(k)]]
+    loc["mod"] = np.where(loc["mod"] >= 0, loc["lt"], loc["mod"])
+    vis = loc["mod"] >= 0
+    case["c0"] = int(loc["lt"][vis].max())
+    return case
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+@pytest.mark.parametrize("seed", [91, 92])
+def test_sorted_packed_frame_edges(gpu_device, monkeypatch, seed, packed):
+    """Order-free sorted path, packed resolve (CRDT_PACKED=1) and its list form (0), on local rows
+    at every edge of the records' frame; one- and two-level capacities."""
+    monkeypatch.setenv("CRDT_PACKED", packed)
+    case = _frame_edge_case(seed)
+    for cap in (None, (1 << 20) + 3):
+        res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap)
+        assert res["path"] == "sorted"
+
+
+def test_sorted_wide_frame_takes_list_form(gpu_device):
+    """Records whose lt span exceeds the packed key (old echoes near lt 0 beside current clocks):
+    the packed kernels exit and the list form resolves the window — same rows as the oracle."""
+    case = make_case(seed=93, R=30, per_cs=1500, n_local=2500, n_new=1500, millis_span=6, counter_span=3,
+                     n_ranks=11, tomb_frac=0.1)
+    rng = np.random.default_rng(93)
+    old = rng.random(len(case["lt"])) < 0.05
+    case["lt"] = np.where(old, rng.integers(1, 1 << 20, len(case["lt"])), case["lt"]).astype(np.int64)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 9)
+    assert res["path"] == "sorted"
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+def test_sorted_split_hot_bucket_packed(gpu_device, monkeypatch, packed):
+    """The split-bucket parts of the packed form (k_resolve_packed<true> + k_part_carry_packed)
+    against the list form's, on the hot-bucket case (4 parts, ties, tombstones)."""
+    monkeypatch.setenv("CRDT_PACKED", packed)
+    case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                     n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False)
+    assert res["path"] == "sorted"
+
+
 def test_sorted_key_out_of_range(gpu_device):
     from crdt_amd import CrdtNativeError, DeviceTable
     t = DeviceTable(0, local_rank=0, capacity=64)
