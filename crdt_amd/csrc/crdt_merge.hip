@@ -1693,9 +1693,11 @@ bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* wi
         if (nw >= (1ull << 31)) return false;
     }
     if (c->merge_path == 2) return true;
-    // auto: many small changesets (cfg3-like fan-in), where one partitioned pass beats R
-    // latency-bound K2 launches; large changesets keep K2 (measured)
-    return R >= 64 && n >= (8ull << 20) && n / R <= (256ull << 10);
+    // auto: a many-changeset fan-in.  Order-free (no per-record counts): the partitioned passes
+    // beat R K2 launches from 64 changesets and 8M records on (1B fan-in: 31.4 vs 34.1 ms,
+    // DESIGN.md §5); with exact counts only while changesets are small (cfg3), where K2's
+    // launches are latency-bound
+    return R >= 64 && n >= (8ull << 20) && (!c->counts || n / R <= (256ull << 10));
 }
 
 // Apply phase over columns whose changeset segments are c->segs (n = column length).

@@ -449,3 +449,101 @@ def test_to_json_encoders_and_int_keys_take_restatement(gpu_device):
     assert s.last_export == "python"
     assert s.toJson() == f'{{"k":{{"hlc":"{Hlc(WALL, 0, "a")}","value":1}}}}'
     assert s.last_export == "native"
+
+
+# ------------------------------------------------------------ parity edges (round 2)
+def _state_equal(dev, ora):
+    rm_d, rm_o = dev.recordMap(), ora.record_map()
+    assert list(rm_d) == list(rm_o)
+    for k in rm_o:
+        assert (rm_d[k].hlc.logicalTime, rm_d[k].hlc.nodeId, rm_d[k].value, rm_d[k].modified.logicalTime) == \
+            (rm_o[k].hlc.logical_time, rm_o[k].hlc.node_id, rm_o[k].value, rm_o[k].modified.logical_time), k
+    assert dev.canonicalTime.logicalTime == ora.canonical_time.logical_time
+
+
+@pytest.mark.parametrize("via", ["merge", "mergeJson"])
+@pytest.mark.parametrize("first", ["\U0001F600", "～"])
+def test_node_ids_ordered_by_utf16_not_utf8(gpu_device, via, first):
+    """hlc.dart:158-161 breaks (lt) ties with String.compareTo: UTF-16 code units.  '😀' (U+1F600,
+    surrogates D83D DE00) sorts BEFORE '～' (U+FF5E) in UTF-16 but after it in UTF-8 bytes and in
+    code points; the same keys at the same lt from both nodes must resolve like the oracle."""
+    from oracle import crdt_oracle as O
+    second = "～" if first == "\U0001F600" else "\U0001F600"
+    dev, ora = MapCrdt("local"), O.MapCrdt("local")
+    for node in (first, second):
+        recs = {f"k{i}": O.Record(O.Hlc(WALL - 10, i % 3, node), f"{node}{i}", O.Hlc(0, 0, "local")) for i in range(12)}
+        if via == "merge":
+            dev.merge({k: Record(Hlc(r.hlc.millis, r.hlc.counter, node), r.value, Hlc(0, 0, "local"))
+                       for k, r in recs.items()}, wall=WALL)
+        else:
+            dev.mergeJson(O.CrdtJson.encode(recs), wall=WALL)
+        ora.merge(recs, WALL) if via == "merge" else ora.merge_json(O.CrdtJson.encode(recs), WALL)
+    _state_equal(dev, ora)
+    assert {r.hlc.nodeId for r in dev.recordMap().values()} == {"～"}     # the UTF-16 larger one
+
+
+def test_parsed_counter_over_0xffff_roundtrip(gpu_device):
+    """An Hlc whose counter exceeds 0xFFFF (Hlc.parse of a wider hex counter, hlc.dart:39-46; lt =
+    (millis << 16) + counter carries into millis, hlc.dart:16): merged, exported with toJson
+    (Hlc.toString keeps millis and counter, hlc.dart:102-104), merged again into a fresh replica."""
+    from oracle import crdt_oracle as O
+    doc_in = '{"a":{"hlc":"%s-1FFFF-zz","value":1},"b":{"hlc":"%s-0003-zz","value":2}}' % (
+        O.iso_from_millis(WALL - 5), O.iso_from_millis(WALL - 5))
+    dev, ora = MapCrdt("local"), O.MapCrdt("local")
+    dev.mergeJson(doc_in, wall=WALL)
+    ora.merge_json(doc_in, WALL)
+    _state_equal(dev, ora)
+    out_d, out_o = dev.toJson(), ora.to_json()
+    assert out_d == out_o and "-1FFFF-zz" in out_d
+    dev2, ora2 = MapCrdt("other"), O.MapCrdt("other")
+    dev2.mergeJson(out_d, wall=WALL)
+    ora2.merge_json(out_o, WALL)
+    _state_equal(dev2, ora2)
+    assert dev2.toJson() == ora2.to_json()
+
+
+@pytest.mark.parametrize("drift_at", [1, 2, 5])
+def test_batch_with_wide_counter_then_normal_records(gpu_device, drift_at):
+    """A changeset whose FIRST record is an Hlc with counter 0x1FFFF, followed by canonical-form
+    records, one of them drifting (millis = wall + 60001): the device's millis column must hold
+    every record's Hlc.millis (it was built from a half-filled lt column)."""
+    from oracle import crdt_oracle as O
+    dev, ora = MapCrdt("local"), O.MapCrdt("local")
+    cs_d, cs_o = {}, {}
+    for i in range(8):
+        if i == 0:
+            ms, cnt = WALL - 3, 0x1FFFF
+        elif i == drift_at:
+            ms, cnt = WALL + 60_001, 0
+        else:
+            ms, cnt = WALL - 1, i
+        cs_d[f"k{i}"] = Record(Hlc(ms, cnt, "peer"), i, Hlc(0, 0, "local"))
+        cs_o[f"k{i}"] = O.Record(O.Hlc(ms, cnt, "peer"), i, O.Hlc(0, 0, "local"))
+    e1 = e2 = None
+    try:
+        dev.mergeAll([{"x": Record(Hlc(WALL - 9, 0, "peer"), 0, Hlc(0, 0, "local"))}, cs_d], wall=WALL)
+    except Exception as ex:  # noqa: BLE001
+        e1 = (type(ex).__name__, str(ex))
+    try:
+        ora.merge({"x": O.Record(O.Hlc(WALL - 9, 0, "peer"), 0, O.Hlc(0, 0, "local"))}, WALL)
+        ora.merge(cs_o, WALL)
+    except Exception as ex:  # noqa: BLE001
+        e2 = (type(ex).__name__, str(ex))
+    assert e1 == e2 and e1 is not None and e1[0] == "ClockDriftException"
+    _state_equal(dev, ora)
+
+
+def test_c_abi_from_a_plain_c_host(gpu_device):
+    """tests/c/abi_golden.c (built by build()): the library loaded by a C program with no Python
+    or torch in it — golden cases through crdt_merge (gather + flags, sorted, and a 1-rank sharded
+    ctx over a loopback crdt_comm_ops table written in C), every row compared bit for bit."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "c", "abi_golden")
+    assert os.path.exists(exe), "build() compiles tests/c/abi_golden"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PYTHON")}
+    out = subprocess.run([exe, os.path.join(root, "tests", "golden", "abi_cases.bin")], capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "all equal" in out.stdout
