@@ -663,12 +663,15 @@ __global__ __launch_bounds__(kScanThreads) void k_route_count(
     }
 }
 
+// kPk: the global record frame fits the sorted path's packed key, so a routed record is 16 B
+// {slot, packed (lt, rank, window changeset) in o_lt, val} instead of 20 B (o_rank unused).
+template <bool kPk>
 __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
     uint32_t jbase, uint32_t R, uint32_t G, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ o_slot,
     int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank, uint32_t* __restrict__ o_val,
-    uint64_t* __restrict__ o_perm)
+    uint64_t* __restrict__ o_perm, PackFrame pf)
 {
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
@@ -701,14 +704,31 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
             if (i < end) {
                 const uint64_t o = s_base[dst[q]] + pos[q];
                 o_slot[o] = k[q] / G;
-                o_lt[o] = __builtin_nontemporal_load(lt + i);
-                o_rank[o] = __builtin_nontemporal_load(rank + i);
+                const int64_t l = __builtin_nontemporal_load(lt + i);
+                const uint32_t r = __builtin_nontemporal_load(rank + i);
+                if (kPk) {
+                    o_lt[o] = (int64_t)pack_record(pf, l, r, j % kWindow);
+                } else {
+                    o_lt[o] = l;
+                    o_rank[o] = r;
+                }
                 o_val[o] = __builtin_nontemporal_load(val + i);
                 if (o_perm) o_perm[o] = i;
             }
         }
         __syncthreads();
     }
+}
+
+// Packed routed records back to (lt, rank) columns, for an apply that takes the gather path.
+__global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt, uint32_t* __restrict__ rank,
+                                                       uint64_t n, PackFrame pf)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t x = (uint64_t)lt[i];
+    lt[i] = (int64_t)((uint64_t)pf.lt0 + (x >> pf.sh));
+    rank[i] = pf.rk0 + (uint32_t)((x >> 13) & pf.rk_mask);
 }
 
 // Win flags of the sent records (send order, returned by the owners) -> batch order.
@@ -1113,10 +1133,11 @@ int stage(crdt_ctx* c, DBuf<T>& buf, const T* src, uint64_t n, int32_t mem, cons
 
 struct Cols {
     const uint32_t* key = nullptr;
-    const int64_t* lt = nullptr;
+    const int64_t* lt = nullptr;       // packed_in: the packed (lt, rank, window changeset) keys
     const uint32_t* rank = nullptr;
     const uint32_t* val = nullptr;
     const int64_t* millis = nullptr;
+    bool packed_in = false;            // records routed in packed (comm_path.inc), for the sorted path
 };
 
 int validate_batch(const crdt_batch* b) {
@@ -1511,11 +1532,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     // batch fits the 64-bit key (one read-back of Misc per call), else wide payloads + lists
     PackFrame pf{};
     bool pk = false;
-    if (!c->counts && c->packed_resolve && c->frame_on) {
+    if (cols.packed_in || (!c->counts && c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         pf = make_frame(c->h_misc->fr_lo, c->h_misc->fr_hi, c->h_misc->fr_rlo, c->h_misc->fr_rhi);
         pk = pf.ok;
+        if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
     c->last_packed = pk;
     for (size_t sb = 0; sb < ns_all;) {
@@ -1582,7 +1604,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
-        if (pk)
+        if (cols.packed_in)
+            k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                c->p1_kj.p, xper1, pf);
+        else if (pk)
             k_part_scatter1<true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
                 c->p1_kj.p, xper1, pf);

@@ -317,6 +317,15 @@ def test_two_rank_routed_sorted_path(gpu_device, counts):
     assert all(o[1]["path"] == "sorted" for o in outs)
 
 
+@pytest.mark.parametrize("kind", ["routed", "parts"])
+@pytest.mark.parametrize("name", ["r4_ties", "drift_late", "send_overflow", "explicit_millis"])
+def test_two_rank_packed_wire_gather_receiver(gpu_device, name, kind):
+    """Order-free merge without win flags: the global frame fits, so records cross as 16-B packed
+    {slot, key, val}; these batches are small, so each owner applies them on the gather path and
+    unpacks (lt, rank) first (k_unpack_routed)."""
+    run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path="auto", counts=False)
+
+
 @pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
 @pytest.mark.parametrize("name", ["r8_tombstones", "drift_late"])
 def test_rccl_single_rank(gpu_device, name, kind):
