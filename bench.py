@@ -138,6 +138,9 @@ def main():
     # per-record n_present / n_won are library extras (not reference results); without them the
     # sorted path folds each bucket in any order (same rows / canonical / status)
     table.set_counts(args.exact_counts)
+    # node ranks are dense host-interned ids (replica j is rank j + 1, local rows 0 .. R): the
+    # sorted path takes its packed key's rank frame from this bound instead of a pass over ranks
+    table.set_rank_bound(wl["R"] + 1 if args.config in ("fanin", "cfg3") else 0)
     if world > 1:
         if backend == "nccl":
             attach_rccl(table, dist)                 # RCCL communicator inside the ctx

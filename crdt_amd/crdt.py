@@ -130,8 +130,11 @@ class MapCrdt(Crdt):
         self._hlc_override: dict = {}     # key id -> Hlc not in canonical (millis, counter) form
         self._mod_override: dict = {}     # key id -> modified Hlc with a foreign node / odd form
         self._watches: list = []
+        self._rank_bound = 0
         self._nodes.register([nodeId])
         self._table = DeviceTable(device, local_rank=self._nodes.rank(nodeId), capacity=capacity)
+        self._table.set_rank_bound(len(self._nodes))
+        self._rank_bound = len(self._nodes)
         self.refreshCanonicalTime()
         if seed:
             self._store(list(seed.items()), notify=False)
@@ -142,6 +145,9 @@ class MapCrdt(Crdt):
         if lut is not None:
             self._table.remap_ranks(len(self._keys), lut)
             self._table.local_rank = self._nodes.rank(self.nodeId)
+        if len(self._nodes) != self._rank_bound:      # ranks are dense: 0 .. len - 1
+            self._rank_bound = len(self._nodes)
+            self._table.set_rank_bound(self._rank_bound)
 
     def _reserve(self):
         if len(self._keys) > self._table.capacity:

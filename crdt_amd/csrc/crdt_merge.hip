@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     int64_t wall, uint32_t local_rank,
     int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
 {
-    static_assert(kEager || !kFrame, "the frame needs every rank");
+    // (kFrame without kEager: the lt frame only — the host declared a rank bound, crdt_set_rank_bound)
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
     __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
@@ -208,9 +208,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                     const uint64_t o = ord64(v[q]);
                     flo = ~o > flo ? ~o : flo;
                     fhi = o > fhi ? o : fhi;
-                    const uint32_t r = rk[kEager ? q : 0];
-                    frl = (uint32_t)~r > frl ? (uint32_t)~r : frl;
-                    frh = r > frh ? r : frh;
+                    if (kEager) {
+                        const uint32_t r = rk[kEager ? q : 0];
+                        frl = (uint32_t)~r > frl ? (uint32_t)~r : frl;
+                        frh = r > frh ? r : frh;
+                    }
                 }
             }
 #pragma unroll
@@ -1072,6 +1074,8 @@ struct crdt_ctx {
     bool xcd_map = true;            // XCD-contiguous tile order in the partition scatters (CRDT_XCD_MAP=0: off)
     bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
+    uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
+    bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
     bool last_packed = false;       // the last sorted apply used the packed form
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
@@ -1223,8 +1227,10 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 // k_clock<true> and the resolve kernels into the last k_verify<true> workgroup (c->fused).
 // frame: also reduce the records' lt / rank frame into misc->fr_* (the sorted path's packed key;
 // the scan then reads every rank with its lt).
+// bound_ok: the frame's rank part may come from crdt_set_rank_bound (single ctx; a sharded merge
+// reduces the ranks' own frame, which the packed wire records are encoded against).
 int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false,
-               bool frame = false) {
+               bool frame = false, bool bound_ok = true) {
     c->fused = false;
     c->resolved = false;
     int st = validate_batch(home);
@@ -1249,6 +1255,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     c->plan_tiles = tiles;
     c->plan_mt = mt;
     c->frame_on = frame;
+    c->frame_lt_only = frame && bound_ok && c->rank_bound && !c->scan_eager;
     c->fused = allow_fuse && !c->no_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
@@ -1256,7 +1263,11 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (frame && !cols.millis)
+            if (c->frame_lt_only)                         // lt frame only: ranks loaded lazily as usual
+                k_scan<false, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+            else if (frame && !cols.millis)
                 k_scan<true, false, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
@@ -1363,6 +1374,19 @@ int kv_copy_all(crdt_ctx* c) {
 
 int comm_all_reduce(crdt_ctx* c, long long* d, uint64_t n, int32_t op);   // comm_path.inc
 
+// The sorted path's frame from the scan's accumulators (read back into h_misc); with a declared
+// rank bound its rank part is [0, bound) — the level-1 scatter checks every rank against it.
+PackFrame frame_of(const crdt_ctx* c) {
+    const Misc* m = c->h_misc;
+    const bool any = m->fr_lo != 0 || m->fr_hi != 0;
+    const bool bound = c->frame_lt_only;
+    const uint32_t rlo = bound ? (any ? ~0u : 0u) : m->fr_rlo;               // ~min: min 0
+    const uint32_t rhi = bound ? (any ? c->rank_bound - 1 : 0u) : m->fr_rhi;
+    PackFrame f = make_frame(m->fr_lo, m->fr_hi, rlo, rhi);
+    f.rk_limit = bound ? c->rank_bound : UINT32_MAX;
+    return f;
+}
+
 // Read the call's outcome back (one D2H of Misc, the only sync of the apply phase).  On a
 // sharded ctx the per-record counts, the key-range error and "not counted" are SUM-reduced
 // over the ranks first, so every rank returns the same result.
@@ -1393,6 +1417,12 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
     }
     res.n_present = all_counted ? np : UINT64_MAX;
     res.n_won = all_counted ? nw : UINT64_MAX;
+    if (c->h_misc->err & 2u) {                 // a rank at or over crdt_set_rank_bound's bound: the
+        res.status = CRDT_E_INVALID;           // resolve stored nothing, the clock does not move
+        res.canonical_lt = c->canonical;
+        if (out) *out = res;
+        return res.status;
+    }
     if (err) res.status = CRDT_E_KEY_RANGE;
     c->canonical = res.canonical_lt;
     if (out) *out = res;
@@ -1535,7 +1565,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     if (cols.packed_in || (!c->counts && c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        pf = make_frame(c->h_misc->fr_lo, c->h_misc->fr_hi, c->h_misc->fr_rlo, c->h_misc->fr_rhi);
+        pf = frame_of(c);
         pk = pf.ok;
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
@@ -1676,11 +1706,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
             k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
-                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf);
+                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
+                c->d_misc);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
-                d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf);
+                d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
-                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf);
+                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
+                c->d_misc);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -2149,6 +2181,12 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         HIPCHK(hipMemcpy(win_flags, dflags, n, hipMemcpyDeviceToHost));
     collect_timing(c);
     return st;
+}
+
+int crdt_set_rank_bound(crdt_ctx* c, uint32_t bound) {
+    if (!c) return CRDT_E_INVALID;
+    c->rank_bound = bound;
+    return CRDT_OK;
 }
 
 int crdt_set_counts(crdt_ctx* c, int exact) {

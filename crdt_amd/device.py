@@ -273,6 +273,11 @@ class DeviceTable:
         bucket in any order (same rows / canonical / status; both counts reported as 2^64 - 1)."""
         self._check(self._lib.crdt_set_counts(self._ctx, 1 if exact else 0), "crdt_set_counts")
 
+    def set_rank_bound(self, bound: int):
+        """crdt_set_rank_bound: every later rank is < bound (0: no promise).  The sorted path then
+        needs no pass over the ranks for its packed key's frame."""
+        self._check(self._lib.crdt_set_rank_bound(self._ctx, int(bound)), "crdt_set_rank_bound")
+
     def set_merge_path(self, path: str):
         """'auto' | 'gather' | 'sorted' (crdt_set_merge_path): the strategy of later merges."""
         self._check(self._lib.crdt_set_merge_path(self._ctx, self.PATHS[path]), "crdt_set_merge_path")

@@ -238,6 +238,13 @@ int crdt_set_merge_path(crdt_ctx* ctx, int path);
  * (ties on (lt, rank) decided by changeset, the local row first — the same rows, canonical and
  * status) and reports both counts as UINT64_MAX; the gather path still counts. */
 int crdt_set_counts(crdt_ctx* ctx, int exact);
+/* A promise that every node-id rank in later batches is < bound (the host interns node ids
+ * densely; 0 = no promise, the default).  The sorted path then takes the rank part of its packed
+ * key's frame from the bound instead of reading every rank in the scan.  A batch that breaks the
+ * promise is never merged wrongly: where the bound is used (a single ctx's packed sorted form) the
+ * call returns CRDT_E_INVALID having stored nothing and left the canonical clock as it was (the
+ * check runs before any row is written); elsewhere the bound is ignored and the merge is exact. */
+int crdt_set_rank_bound(crdt_ctx* ctx, uint32_t bound);
 int crdt_last_path(const crdt_ctx* ctx, int* path);
 
 /* ---- measurement ---------------------------------------------------------- */

@@ -12,16 +12,19 @@ RESULT_FIELDS = ("status", "n_stored", "exc_changeset", "exc_index", "canonical_
                  "n_present", "n_won")
 
 
-def device_run(case, device_cols=False, capacity=None, path=None, flags=True, counts=True):
+def device_run(case, device_cols=False, capacity=None, path=None, flags=True, counts=True, rank_bound=0):
     """path: None (auto) | 'gather' | 'sorted' (crdt_set_merge_path); flags=False asks for no
     per-record win flags (the sorted path's precondition), returned flags are then None;
-    counts=False: crdt_set_counts(0) (the sorted path's order-free form)."""
+    counts=False: crdt_set_counts(0) (the sorted path's order-free form); rank_bound:
+    crdt_set_rank_bound."""
     from crdt_amd import DeviceTable
     t = DeviceTable(0, local_rank=case["local_rank"], capacity=capacity or case["n_ids"])
     if path:
         t.set_merge_path(path)
     if not counts:
         t.set_counts(False)
+    if rank_bound:
+        t.set_rank_bound(rank_bound)
     loc = case["local"]
     keep = loc["mod"] != ABSENT_MOD
     ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
@@ -566,6 +569,59 @@ def test_sorted_packed_frame_edges(gpu_device, monkeypatch, seed, packed):
     for cap in (None, (1 << 20) + 3):
         res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap)
         assert res["path"] == "sorted"
+
+
+@pytest.mark.parametrize("slack", [0, 1, 700])
+@pytest.mark.parametrize("seed", [91, 92])
+def test_sorted_rank_bound_frame(gpu_device, seed, slack):
+    """crdt_set_rank_bound: the packed frame's rank part comes from the bound (the scan reads lt
+    only) — tight and loose bounds, local rows with ranks above it, same rows as the oracle."""
+    case = _frame_edge_case(seed)
+    bound = int(case["rank"].max()) + 1 + slack
+    for cap in (None, (1 << 20) + 3):
+        res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound)
+        assert res["path"] == "sorted"
+
+
+@pytest.mark.parametrize("counts", [False, True])
+def test_rank_bound_violation_stores_nothing(gpu_device, counts):
+    """A batch rank at or above the promised bound: the packed sorted form refuses the call with
+    CRDT_E_INVALID before writing a row (canonical unchanged); the counted form does not use the
+    bound and merges exactly."""
+    from crdt_amd import CrdtNativeError, DeviceTable
+    case = make_case(seed=94, R=20, per_cs=1000, n_local=2000, n_new=500, millis_span=4, counter_span=2,
+                     n_ranks=9, tomb_frac=0.1)
+    bound = int(case["rank"].max())               # the highest rank breaks the promise
+    if counts:
+        res = compare_with_oracle(case, path="sorted", flags=False, counts=True, rank_bound=bound)
+        assert res["status"] == 0
+        return
+    t = DeviceTable(0, local_rank=case["local_rank"], capacity=case["n_ids"])
+    t.set_merge_path("sorted")
+    t.set_counts(False)
+    t.set_rank_bound(bound)
+    loc = case["local"]
+    keep = loc["mod"] != ABSENT_MOD
+    ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
+    t.put_rows(ids, loc["lt"][keep], loc["rank"][keep], loc["val"][keep], loc["mod"][keep])
+    t.canonical = case["c0"]
+    before = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
+    with pytest.raises(CrdtNativeError, match="invalid"):
+        t.merge(case["key"], case["lt"], case["rank"], case["val"], case["offsets"], case["wall"],
+                millis=case["millis"], win_flags=False)
+    assert t.last_path() == "sorted"
+    after = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
+    for a, b in zip(before, after):
+        assert np.array_equal(a, b)
+    assert t.canonical == case["c0"]
+    t.set_rank_bound(0)                           # promise withdrawn: the same batch merges exactly
+    res, _ = t.merge(case["key"], case["lt"], case["rank"], case["val"], case["offsets"], case["wall"],
+                     millis=case["millis"], win_flags=False)
+    orows, ores, _ = oracle_run(case)
+    for f, a in zip(("lt", "rank", "val", "mod"), t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))):
+        assert np.array_equal(a, orows[f]), f
+    assert res["canonical_lt"] == ores["canonical_lt"]
+    t.close()
 
 
 def test_sorted_wide_frame_takes_list_form(gpu_device):
