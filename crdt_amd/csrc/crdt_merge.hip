@@ -137,6 +137,25 @@ __device__ inline int64_t wave_scan_max_incl(int64_t v, int lane) {
     return v;
 }
 
+// Add this lane's record to bin d (if act) and return its slot among the records of bin d
+// counted so far (arbitrary order inside one call).  The lanes sharing the first active lane's
+// digit take one atomic together (all of a single-digit wave; most of a skewed one, where one
+// hot digit would otherwise serialise on its LDS address), every other lane one of its own.
+__device__ inline uint32_t digit_count(uint32_t* bins, uint32_t d, bool act, int lane) {
+    const unsigned long long a = __ballot(act);
+    if (!a) return 0;
+    const int L = __ffsll((long long)a) - 1;
+    const uint32_t d0 = __shfl(d, L, 64);
+    const bool same = act && d == d0;
+    const unsigned long long m = __ballot(same);
+    const unsigned long long below = (1ull << lane) - 1;
+    uint32_t base = 0;
+    if (lane == L) base = atomicAdd(&bins[d0], (uint32_t)__popcll(m));
+    base = __shfl(base, L, 64);
+    if (same) return base + (uint32_t)__popcll(m & below);
+    return act ? atomicAdd(&bins[d], 1u) : 0u;
+}
+
 // =============================================================================
 // K3a — k_scan: M_j = max lt of changeset j; tiles that may raise in recv().
 // A record can raise only if it is flagged (rank == local: DuplicateNode,
@@ -155,38 +174,69 @@ __host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ul
 // kFrame (the sorted path will run): with rank loaded eagerly, also the frame of the records
 // (lt and rank bounds) into misc->fr_*, one set of atomics per workgroup and tile, only where
 // it moves a bound (a stale read of a bound never makes a needed atomic look useless)
-template <bool kEager, bool kMillis = true, bool kFrame = false>
+// kHist (the sorted path's level-1 histogram fused into the scan, single ctx, one window): the
+// keys are read with lt and counted per level-1 partition tile (kHistSub scan tiles, never
+// straddling a changeset) into hist[ptb[j] + u][256] — what k_part_hist<true> would write with
+// every changeset applied (tiles of changesets >= stop are zeroed once stop is known).
+constexpr uint32_t kHistSub = 8;                 // scan tiles per level-1 partition tile
+struct ScanHist {
+    const uint32_t* key;
+    const uint32_t* ptb;        // [R + 1] first partition tile of changeset j
+    uint64_t cap;
+    uint32_t shift;
+    uint32_t* hist;
+};
+
+template <bool kEager, bool kMillis = true, bool kFrame = false, bool kHist = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
     int64_t wall, uint32_t local_rank,
-    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile)
+    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh)
 {
     // (kFrame without kEager: the lt frame only — the host declared a rank bound, crdt_set_rank_bound)
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
     __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
+    __shared__ uint32_t s_h[kHist ? 256 : 1];
+    static_assert(!kHist || kScanThreads == 256, "one histogram bin per thread");
     const uint32_t j = jbase + blockIdx.y;
     const uint64_t beg = offs[j], end = offs[j + 1];
     const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    constexpr uint32_t kStep = kHist ? kHistSub : 1u;
+    for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
+      if (kHist) {
+        s_h[threadIdx.x] = 0;
+        __syncthreads();
+      }
+      const uint32_t te = std::min<uint32_t>(u * kStep + kStep, nt);
+      for (uint32_t t = u * kStep; t < te; ++t) {
         const uint64_t base = beg + (uint64_t)t * kTile;
         int64_t m = INT64_MIN;
         int f = 0;
         int64_t v[kScanItems];
         uint32_t rk[kEager ? kScanItems : 1];
         int64_t mv[kEager && kMillis ? kScanItems : 1];
+        uint32_t kk[kHist ? kScanItems : 1];
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
             v[q] = i < end ? lt[i] : INT64_MIN;
+            if (kHist) kk[kHist ? q : 0] = i < end ? __builtin_nontemporal_load(sh.key + i) : UINT32_MAX;
             if (kEager) {
                 rk[q] = i < end ? rank[i] : 0u;
                 if (kMillis) mv[kMillis ? q : 0] = (millis && i < end) ? millis[i] : 0;
             }
             m = imax(m, v[q]);
+        }
+        if (kHist) {
+#pragma unroll
+            for (int q = 0; q < kScanItems; ++q) {
+                const uint32_t k = kk[kHist ? q : 0];
+                digit_count(s_h, (k >> sh.shift) & 255u, k < sh.cap, lane);
+            }
         }
         // rank / millis matter only for records above C0 (the only ones recv() can raise on)
 #pragma unroll
@@ -251,6 +301,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             if ((tf & 2) && ((t0 + t) & (kHotSample - 1)) == 0) atomicAdd(&misc->tiles_hot, 1u);   // sampled
         }
         __syncthreads();
+      }
+      if (kHist) sh.hist[(uint64_t)(sh.ptb[j] + u) * 256 + threadIdx.x] = s_h[threadIdx.x];
     }
 }
 
@@ -1075,7 +1127,16 @@ struct crdt_ctx {
     bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
+    bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
+    bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
+    // level-1 histogram counted by the scan (k_scan<.., kHist>) for the sorted path of this plan
+    const uint32_t* d_ptb = nullptr;
+    uint64_t plan_ptiles = 0;
+    DBuf<uint32_t> p_hist1;
+    bool hist1_fused = false;
+    const uint32_t* hist1_key = nullptr;
+    uint32_t hist1_shift = 0;
     bool last_packed = false;       // the last sorted apply used the packed form
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
@@ -1181,20 +1242,25 @@ int stage_apply_cols(crdt_ctx* c, const crdt_batch* b, Cols* cols) {
 // Upload offsets + per-changeset tile starts; returns total tiles and max tiles.
 int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t* max_tiles) {
     const uint32_t R = b->n_changesets;
-    const size_t words = (R + 1) + (R + 2) / 2;          // u64 words: offsets, then packed u32 starts
+    // u64 words: offsets, then packed u32 scan-tile starts and level-1 partition-tile starts
+    const size_t half = (R + 2) / 2;
+    const size_t words = (R + 1) + 2 * half;
     HIPALLOC(c->h_plan.ensure(words));
     HIPALLOC(c->d_plan.ensure(words));
     uint64_t* h_offs = c->h_plan.p;
     uint32_t* h_tstart = reinterpret_cast<uint32_t*>(c->h_plan.p + (R + 1));
-    uint64_t tiles = 0;
+    uint32_t* h_ptb = reinterpret_cast<uint32_t*>(c->h_plan.p + (R + 1) + half);
+    uint64_t tiles = 0, ptiles = 0;
     uint32_t mt = 0;
     for (uint32_t j = 0; j <= R; ++j) {
         h_offs[j] = b->offsets[j];
         h_tstart[j] = (uint32_t)tiles;
+        h_ptb[j] = (uint32_t)ptiles;
         if (j < R) {
             const uint64_t nj = b->offsets[j + 1] - b->offsets[j];
             const uint64_t tj = (nj + kTile - 1) / kTile;
             tiles += tj;
+            ptiles += (tj + kHistSub - 1) / kHistSub;
             mt = std::max<uint32_t>(mt, (uint32_t)tj);
         }
     }
@@ -1202,6 +1268,8 @@ int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t*
     HIPCHK(hipMemcpyAsync(c->d_plan.p, c->h_plan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     c->d_offs = c->d_plan.p;
     c->d_tstart = reinterpret_cast<const uint32_t*>(c->d_plan.p + (R + 1));
+    c->d_ptb = reinterpret_cast<const uint32_t*>(c->d_plan.p + (R + 1) + half);
+    c->plan_ptiles = ptiles;
     *tiles_out = tiles;
     *max_tiles = mt;
     return CRDT_OK;
@@ -1230,9 +1298,10 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 // bound_ok: the frame's rank part may come from crdt_set_rank_bound (single ctx; a sharded merge
 // reduces the ranks' own frame, which the packed wire records are encoded against).
 int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false,
-               bool frame = false, bool bound_ok = true) {
+               bool frame = false, bool bound_ok = true, bool keys_ready = false) {
     c->fused = false;
     c->resolved = false;
+    c->hist1_fused = false;
     int st = validate_batch(home);
     if (st) return st;
     const uint32_t R = home->n_changesets;
@@ -1257,36 +1326,53 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     c->frame_on = frame;
     c->frame_lt_only = frame && bound_ok && c->rank_bound && !c->scan_eager;
     c->fused = allow_fuse && !c->no_fuse && tiles > 0 && tiles <= kClockTilesMax && R <= kClockRMax;
+    // the sorted path's level-1 histogram rides on the scan when the keys are device-resident
+    // (no staging copy of them here) and the call is one window of changesets (sorted_path.inc)
+    // (a host batch arrives here as device columns whose keys are still being copied: keys_ready)
+    const bool hist = c->frame_lt_only && c->hist_fuse && keys_ready && home->mem == CRDT_MEM_DEVICE &&
+                      R <= kWindow && tiles > 0 && home->key_id;
+    if (hist) {
+        HIPALLOC(c->p_hist1.ensure(c->plan_ptiles * kDigits));
+        c->hist1_fused = true;
+        c->hist1_key = home->key_id;
+        c->hist1_shift = c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
+    }
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
         const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
+        const uint32_t gxh = std::max<uint32_t>(1, std::min<uint32_t>((mt + kHistSub - 1) / kHistSub, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (c->frame_lt_only)                         // lt frame only: ranks loaded lazily as usual
+            if (hist)
+                k_scan<false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
+                    ScanHist{home->key_id, c->d_ptb, c->cap, c->hist1_shift, c->p_hist1.p});
+            else if (c->frame_lt_only)                    // lt frame only: ranks loaded lazily as usual
                 k_scan<false, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
             else if (frame && !cols.millis)
                 k_scan<true, false, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
             else if (frame)
                 k_scan<true, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
             else if (c->scan_eager && !cols.millis)
                 k_scan<true, false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
             else if (c->scan_eager)
                 k_scan<true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
             else
                 k_scan<false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
         }
         if (!c->fused)
             k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);
@@ -1570,6 +1656,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
     c->last_packed = pk;
+    c->last_hist1_fused = false;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -1628,11 +1715,21 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tail),
                           reinterpret_cast<const uint32_t*>(c->p_plan.p + tail + 1), c->p_plan.p + tail + 2, 1};
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
-        k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1, c->p_hist.p);
-        k_scan_part<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, sm1, c->p_part.p);
+        // level-1 histogram: counted by the scan (then only the changesets >= stop are cleared)
+        // or here
+        const bool h1 = c->hist1_fused && s0 == 0 && se == ns_all && !cols.packed_in && cols.key == c->hist1_key &&
+                        c->hist1_shift == shift1 && nt1 == c->plan_ptiles;
+        const uint32_t* hist1 = h1 ? c->p_hist1.p : c->p_hist.p;
+        if (h1)
+            k_hist_trim<<<256, 256, 0, c->stream>>>(c->p_hist1.p, c->d_ptb, R, c->d_misc);
+        else
+            k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1,
+                                                                 c->p_hist.p);
+        c->last_hist1_fused = h1;
+        k_scan_part<<<nc1, 256, 0, c->stream>>>(hist1, sm1, c->p_part.p);
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
-        k_scan_tiles<<<nc1, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
+        k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         if (cols.packed_in)
             k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
@@ -1855,6 +1952,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
@@ -1899,7 +1997,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->d_word.release();
     c->d_ibase.release();
     c->p1_rec.release(); c->p1_kj.release(); c->p2_rec.release(); c->p2_kj.release();
-    c->p_hist.release(); c->p_toff.release(); c->p_part.release(); c->p_choff.release();
+    c->p_hist.release(); c->p_hist1.release(); c->p_toff.release(); c->p_part.release(); c->p_choff.release();
     c->p_dstart1.release(); c->p_dstart2.release(); c->p_l2map.release();
     c->p_plan.release(); c->p_l1beg.release(); c->h_pplan.release();
     c->p_ibase.release(); c->p_ksu32.release(); c->p_kslt.release(); c->p_tseg.release();
@@ -2167,7 +2265,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     c->segs.from_offsets(batch->offsets, R);
     const bool frame = !c->counts && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
     ev_record(c, kEvStart);
-    if ((st = phase_scan(c, &dev, wall, c->d_M.p, true, frame))) return st;
+    if ((st = phase_scan(c, &dev, wall, c->d_M.p, true, frame, true, batch->mem == CRDT_MEM_DEVICE))) return st;
     ev_record(c, kEvScan);
     if ((st = phase_clock(c, &dev, wall, c->d_M.p, c->d_event.p))) return st;
     if (!c->resolved && (st = phase_resolve(c, c->d_event.p))) return st;
@@ -2204,6 +2302,19 @@ int crdt_set_merge_path(crdt_ctx* c, int path) {
 int crdt_last_path(const crdt_ctx* c, int* path) {
     if (!c || !path) return CRDT_E_INVALID;
     *path = c->last_sorted ? CRDT_PATH_SORTED : CRDT_PATH_GATHER;
+    return CRDT_OK;
+}
+
+int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
+    if (!c || !flags) return CRDT_E_INVALID;
+    uint32_t f = 0;
+    if (c->last_sorted) {
+        f |= CRDT_PLAN_SORTED;
+        if (c->last_packed) f |= CRDT_PLAN_PACKED;
+        if (c->cap > (1ull << 20)) f |= CRDT_PLAN_TWO_LEVEL;
+        if (c->last_hist1_fused) f |= CRDT_PLAN_HIST_IN_SCAN;
+    }
+    *flags = f;
     return CRDT_OK;
 }
 

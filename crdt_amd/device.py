@@ -287,6 +287,14 @@ class DeviceTable:
         self._check(self._lib.crdt_last_path(self._ctx, ctypes.byref(v)), "crdt_last_path")
         return {1: "gather", 2: "sorted"}[v.value]
 
+    PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8}
+
+    def last_plan(self) -> dict:
+        """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""
+        v = ctypes.c_uint32(0)
+        self._check(self._lib.crdt_last_plan(self._ctx, ctypes.byref(v)), "crdt_last_plan")
+        return {k: bool(v.value & b) for k, b in self.PLAN_FLAGS.items()}
+
     def set_timing(self, enable: bool):
         self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")
 

@@ -246,6 +246,14 @@ int crdt_set_counts(crdt_ctx* ctx, int exact);
  * check runs before any row is written); elsewhere the bound is ignored and the merge is exact. */
 int crdt_set_rank_bound(crdt_ctx* ctx, uint32_t bound);
 int crdt_last_path(const crdt_ctx* ctx, int* path);
+/* How the last crdt_merge ran (diagnostics for tests and profiles): bit flags. */
+enum crdt_plan_flags {
+    CRDT_PLAN_SORTED = 1,        /* the sorted path ran */
+    CRDT_PLAN_PACKED = 2,        /* ... in its packed order-free form (64-bit keys, sorted_path.inc) */
+    CRDT_PLAN_TWO_LEVEL = 4,     /* ... with two partition levels (capacity > 2^20) */
+    CRDT_PLAN_HIST_IN_SCAN = 8   /* ... with its level-1 histogram counted by the scan */
+};
+int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 
 /* ---- measurement ---------------------------------------------------------- */
 int crdt_set_timing(crdt_ctx* ctx, int enable);

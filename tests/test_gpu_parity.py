@@ -43,6 +43,7 @@ def device_run(case, device_cols=False, capacity=None, path=None, flags=True, co
     lt, rank, val, mod = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
     assert t.canonical == res["canonical_lt"]
     res["path"] = t.last_path()
+    res["plan"] = t.last_plan()
     t.close()
     return (lt, rank, val, mod), res, fl
 
@@ -581,6 +582,41 @@ def test_sorted_rank_bound_frame(gpu_device, seed, slack):
     for cap in (None, (1 << 20) + 3):
         res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound)
         assert res["path"] == "sorted"
+
+
+def _late_drift_case(seed):
+    """A ClockDrift in a late changeset: stop < R, the changesets from it on are not applied."""
+    case = make_case(seed=seed, R=48, per_cs=3000, n_local=4000, n_new=2000, millis_span=4, counter_span=3,
+                     n_ranks=7, tomb_frac=0.1)
+    x = int(case["offsets"][37]) + 5
+    case["lt"][x] = (case["wall"] + 60_001) << 16
+    return case
+
+
+@pytest.mark.parametrize("kind", ["edges", "late_drift", "hot"])
+@pytest.mark.parametrize("cap", [None, (1 << 20) + 3])
+def test_sorted_hist_in_scan(gpu_device, monkeypatch, kind, cap):
+    """The level-1 histogram counted by the scan (device columns, rank bound, order-free form):
+    same rows / result as the oracle and as the separate histogram pass (CRDT_HIST_FUSE=0),
+    including a stop < R (rows of the unapplied changesets' tiles cleared) and one / two levels."""
+    if kind == "edges":
+        case = _frame_edge_case(95)
+    elif kind == "late_drift":
+        case = _late_drift_case(96)
+    else:
+        case = make_case(seed=97, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                         n_ranks=9, tomb_frac=0.2)
+    bound = int(case["rank"].max()) + 1
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound,
+                              device_cols=True)
+    assert res["path"] == "sorted" and res["plan"]["hist_in_scan"], res["plan"]
+    assert res["plan"]["two_level"] == (cap is not None)
+    if kind == "late_drift":
+        assert res["status"] != 0 and res["n_stored"] < len(case["offsets"]) - 1
+    monkeypatch.setenv("CRDT_HIST_FUSE", "0")
+    res0 = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound,
+                               device_cols=True)
+    assert not res0["plan"]["hist_in_scan"]
 
 
 @pytest.mark.parametrize("counts", [False, True])

@@ -18,6 +18,11 @@ for spec in "$@"; do
 import json,sys; d=json.load(open('gpurun_out/bench_$name.json')); print('$name', d['ms_per_step'], d['config']['merge_path'], d['roofline'].get('frac'), d['breakdown_ms'])" || true
   [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_$name.log; exit $rc; }
   last="$envs|$args"
+  if [ "${PROF:-0}" = "all" ]; then   # a kernel trace of every spec, each in its own directory
+    timeout -k 10 400 env $envs rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$name -o run -- python3 bench.py $args --steps 2 --warmup 1 --no-cpu --no-census --no-pcie > gpurun_out/prof_$name.log 2>&1
+    rc=$?; echo "[prof $name] exit $rc"; [ $rc -eq 0 ] || exit $rc
+    f=$(find gpurun_out/prof_$name -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && python3 tools/kstats.py "$f" | head -${PROF_TOP:-12}
+  fi
 done
 if [ "${PROF:-0}" = "1" ] && [ -n "$last" ]; then
   envs=$(echo "$last" | cut -d'|' -f1); args=$(echo "$last" | cut -d'|' -f2-)
