@@ -57,41 +57,45 @@ constexpr int64_t kLowBits = 40;
 constexpr int64_t kLowMask = (1ll << kLowBits) - 1;
 constexpr int64_t kEvNone = INT64_MAX;
 
-// One device row per key id, 32 B, 32-B aligned.  Everything the merge decision
-// needs sits in the first 16 B, so the gather of a row is ONE dwordx4 (random
-// row accesses are request-rate bound: tools/ubench_gather.hip):
-//   [0:8)  lt      Record.hlc.logicalTime
-//   [8:12) rank    Record.hlc.nodeId rank
-//   [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the
-//                  visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
-//   [16:20) mod_lo low word of modified
-//   [20:24) val    Record.value handle
-//   [24:32) aux    reserved (zero)
-struct alignas(32) Row {
+// One device row per key id, split by use into two arrays (structure of arrays):
+//   hot  Row  16 B, 16-B aligned — everything the merge decision reads, so the gather of a row
+//             is ONE dwordx4 (random row accesses are request-rate bound: tools/ubench_gather.hip)
+//             and the sorted path's per-bucket row load reads 64 KB per 4096 keys, all of it used:
+//     [0:8)  lt      Record.hlc.logicalTime
+//     [8:12) rank    Record.hlc.nodeId rank
+//     [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the
+//                    visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
+//   cold RowX  8 B — written with a winning record, read only by the views:
+//     [0:4)  mod_lo  low word of modified
+//     [4:8)  val     Record.value handle
+// (One 32-B row made every bucket load fetch the whole line for its first 16 B and every write
+// cost 32 B: the split takes 8 GB -> 4 GB of row reads and 5.4 -> 4.1 GB of row writes off a
+// 1B-record fan-in over 2^28 keys.)
+struct alignas(16) Row {
     int64_t lt;
     uint32_t rank;
     int32_t mod_hi;
+};
+struct alignas(8) RowX {
     uint32_t mod_lo;
     uint32_t val;
-    int64_t aux;
 };
-static_assert(sizeof(Row) == 32, "row layout");
+static_assert(sizeof(Row) == 16 && sizeof(RowX) == 8, "row layout");
+struct Table {
+    Row* hot;
+    RowX* cold;
+};
 
-__host__ __device__ inline int64_t row_mod(const Row& r) {
-    return (int64_t)(((uint64_t)(uint32_t)r.mod_hi << 32) | r.mod_lo);
+__device__ inline int64_t row_mod(const Table& t, uint64_t k) {
+    return (int64_t)(((uint64_t)(uint32_t)t.hot[k].mod_hi << 32) | t.cold[k].mod_lo);
 }
-__host__ __device__ inline Row make_row(int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
-    Row r;
-    r.lt = lt; r.rank = rank; r.mod_hi = (int32_t)((uint64_t)mod >> 32); r.mod_lo = (uint32_t)mod;
-    r.val = val; r.aux = 0;
-    return r;
-}
-typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
-__device__ inline void store_row(Row* dst, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
-    u32x8 v;                       // one 32-B vector store = two aligned dwordx4
-    v.s0 = (uint32_t)lt; v.s1 = (uint32_t)((uint64_t)lt >> 32); v.s2 = rank; v.s3 = (uint32_t)((uint64_t)mod >> 32);
-    v.s4 = (uint32_t)mod; v.s5 = val; v.s6 = 0u; v.s7 = 0u;
-    *reinterpret_cast<u32x8*>(dst) = v;
+__device__ inline void store_row(const Table& t, uint64_t k, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
+    uint4 h;                       // one dwordx4 + one dwordx2
+    h.x = (uint32_t)lt; h.y = (uint32_t)((uint64_t)lt >> 32); h.z = rank; h.w = (uint32_t)((uint64_t)mod >> 32);
+    *reinterpret_cast<uint4*>(t.hot + k) = h;
+    uint2 x;
+    x.x = (uint32_t)mod; x.y = val;
+    *reinterpret_cast<uint2*>(t.cold + k) = x;
 }
 
 // Device-side per-call words.
@@ -619,7 +623,7 @@ template <int kApplyItems>
 __global__ __launch_bounds__(kApplyThreads) void k_apply(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt,
     const uint32_t* __restrict__ rank, const uint32_t* __restrict__ val, uint64_t beg,
-    uint64_t end, uint32_t j, Row* __restrict__ table, uint64_t cap,
+    uint64_t end, uint32_t j, Table table, uint64_t cap,
     const int64_t* __restrict__ Rj, Misc* __restrict__ misc, uint8_t* __restrict__ flags)
 {
     if (j >= misc->stop) return;                          // uniform: changeset past the stop point
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     for (int q = 0; q < kApplyItems; ++q) {              // all gathers in flight, one dwordx4 each
         ok[q] = in[q] && k[q] < cap;
         const uint64_t row = ok[q] ? k[q] : 0;
-        h[q] = *reinterpret_cast<const uint4*>(table + row);
+        h[q] = *reinterpret_cast<const uint4*>(table.hot + row);
     }
     int npres = 0, nwon = 0;
     bool bad = false;
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
         npres += ok[q] && present;
         nwon += win;
         bad |= in[q] && !ok[q];
-        if (win) store_row(table + k[q], l[q], r[q], v[q], stamp);
+        if (win) store_row(table, k[q], l[q], r[q], v[q], stamp);
         if (flags && in[q]) flags[base + (uint64_t)q * kApplyThreads] = win ? 1 : 0;
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
@@ -860,30 +864,30 @@ __global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long l
 // ----------------------------------------------------------------- SPI kernels
 __global__ __launch_bounds__(256) void k_put_rows(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
-    const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Row* __restrict__ table,
+    const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Table table,
     uint64_t cap, Misc* __restrict__ misc)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    table[k] = make_row(lt[i], rank[i], val[i], mod[i]);
+    store_row(table, k, lt[i], rank[i], val[i], mod[i]);
 }
 
 // put/putAll rows (crdt.dart:41-42, 51-53): hlc = modified = the one send() result.
 __global__ __launch_bounds__(256) void k_put_stamped(
     const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n, int64_t stamp,
-    uint32_t local_rank, Row* __restrict__ table, uint64_t cap, Misc* __restrict__ misc)
+    uint32_t local_rank, Table table, uint64_t cap, Misc* __restrict__ misc)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    table[k] = make_row(stamp, local_rank, val[i], stamp);
+    store_row(table, k, stamp, local_rank, val[i], stamp);
 }
 
 __global__ __launch_bounds__(256) void k_read_rows(
-    const uint32_t* __restrict__ key, uint64_t n, const Row* __restrict__ table, uint64_t cap,
+    const uint32_t* __restrict__ key, uint64_t n, Table table, uint64_t cap,
     int64_t* __restrict__ lt, uint32_t* __restrict__ rank, uint32_t* __restrict__ val,
     int64_t* __restrict__ mod, Misc* __restrict__ misc)
 {
@@ -891,11 +895,11 @@ __global__ __launch_bounds__(256) void k_read_rows(
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    const Row row = table[k];
+    const Row row = table.hot[k];
     if (lt) lt[i] = row.lt;
     if (rank) rank[i] = row.rank;
-    if (val) val[i] = row.val;
-    if (mod) mod[i] = row_mod(row);
+    if (val) val[i] = table.cold[k].val;
+    if (mod) mod[i] = row_mod(table, k);
 }
 
 // refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
@@ -920,7 +924,7 @@ __global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, 
 
 // recordMap(modifiedSince) (map_crdt.dart:42-45): order-preserving compaction.
 constexpr int kMsPerBlock = 1024;
-__global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table, uint64_t n, int64_t since,
+__global__ __launch_bounds__(256) void k_ms_count(Table table, uint64_t n, int64_t since,
                                                   uint32_t* __restrict__ counts)
 {
     __shared__ int s[4];
@@ -928,7 +932,7 @@ __global__ __launch_bounds__(256) void k_ms_count(const Row* __restrict__ table,
     int c = 0;
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        if (i < n) c += !(row_mod(table[i]) < since);
+        if (i < n) c += !(row_mod(table, i) < since);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -975,7 +979,7 @@ __global__ __launch_bounds__(1024) void k_ms_scan(uint32_t* __restrict__ counts,
     if (tid == 0) *total = (long long)s_carry;
 }
 
-__global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table, uint64_t n, int64_t since,
+__global__ __launch_bounds__(256) void k_ms_write(Table table, uint64_t n, int64_t since,
                                                   const uint32_t* __restrict__ offsets,
                                                   uint32_t* __restrict__ out)
 {
@@ -985,7 +989,7 @@ __global__ __launch_bounds__(256) void k_ms_write(const Row* __restrict__ table,
     uint32_t run = offsets[blockIdx.x];
     for (int q = 0; q < kMsPerBlock / 256; ++q) {
         const uint64_t i = base + q * 256 + threadIdx.x;
-        const bool keep = i < n && !(row_mod(table[i]) < since);
+        const bool keep = i < n && !(row_mod(table, i) < since);
         const unsigned long long b = __ballot(keep);
         const int before = __popcll(b & ((1ull << lane) - 1));
         if (lane == 0) s_wave[w] = __popcll(b);
@@ -1068,7 +1072,7 @@ struct crdt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t local_rank = 0;
-    Row* table = nullptr;
+    Table table{nullptr, nullptr};  // hot / cold row arrays, capacity rows each
     uint64_t cap = 0;
     int64_t canonical = 0;
 
@@ -1127,6 +1131,7 @@ struct crdt_ctx {
     bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
+    uint32_t exp = 0;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
     bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
@@ -1804,12 +1809,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
             k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
                 bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
-                c->d_misc);
+                c->d_misc, c->exp);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
                 bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
-                c->d_misc);
+                c->d_misc, c->exp);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -1953,6 +1958,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_EXP")) c->exp = (uint32_t)atoi(e);   // timing experiments: wrong results
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
@@ -1984,7 +1990,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
     c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release();
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
-    if (c->table) hipFree(c->table);
+    if (c->table.hot) hipFree(c->table.hot);
+    if (c->table.cold) hipFree(c->table.cold);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
     c->d_M.release(); c->d_event.release(); c->d_plan.release();
@@ -2011,17 +2018,26 @@ void crdt_destroy(crdt_ctx* c) {
 
 int crdt_reserve(crdt_ctx* c, uint64_t capacity) {
     if (!c) return CRDT_E_INVALID;
-    if (capacity <= c->cap && c->table) return CRDT_OK;
+    if (capacity <= c->cap && c->table.hot) return CRDT_OK;
     if (capacity > (1ull << 32)) return CRDT_E_INVALID;   // key ids are uint32
     HIPCHK(hipSetDevice(c->device));
     const uint64_t newcap = std::max<uint64_t>(capacity, 16);
-    Row* t = nullptr;
-    HIPALLOC(hipMalloc(&t, newcap * sizeof(Row)));
-    if (c->table && c->cap)
-        HIPCHK(hipMemcpyAsync(t, c->table, c->cap * sizeof(Row), hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(hipMemsetAsync(t + c->cap, 0x80, (newcap - c->cap) * sizeof(Row), c->stream));
+    Table t{nullptr, nullptr};
+    HIPALLOC(hipMalloc(&t.hot, newcap * sizeof(Row)));
+    if (hipMalloc(&t.cold, newcap * sizeof(RowX)) != hipSuccess) {
+        hipFree(t.hot);
+        return CRDT_E_NOMEM;
+    }
+    if (c->table.hot && c->cap) {
+        HIPCHK(hipMemcpyAsync(t.hot, c->table.hot, c->cap * sizeof(Row), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(t.cold, c->table.cold, c->cap * sizeof(RowX), hipMemcpyDeviceToDevice, c->stream));
+    }
+    // absent rows: mod_hi 0x80808080 < 0 (and mod = 0x8080808080808080)
+    HIPCHK(hipMemsetAsync(t.hot + c->cap, 0x80, (newcap - c->cap) * sizeof(Row), c->stream));
+    HIPCHK(hipMemsetAsync(t.cold + c->cap, 0x80, (newcap - c->cap) * sizeof(RowX), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->table) hipFree(c->table);
+    if (c->table.hot) hipFree(c->table.hot);
+    if (c->table.cold) hipFree(c->table.cold);
     c->table = t;
     c->cap = newcap;
     return CRDT_OK;
@@ -2159,7 +2175,7 @@ int crdt_refresh_canonical(crdt_ctx* c, uint64_t n_rows, int64_t* out_lt) {
     k_fill_i64<<<1, 64, 0, c->stream>>>(c->d_word.p, 1, INT64_MIN);
     if (n_rows) {
         const unsigned g = std::min<unsigned>(grid_for(n_rows, 256), 2048);
-        k_refresh<<<g, 256, 0, c->stream>>>(c->table, n_rows, c->d_word.p);
+        k_refresh<<<g, 256, 0, c->stream>>>(c->table.hot, n_rows, c->d_word.p);
         HIPCHK(hipGetLastError());
     }
     long long w = 0;
@@ -2196,7 +2212,8 @@ int crdt_clear_rows(crdt_ctx* c, uint64_t first, uint64_t count) {
     if (!c || first > c->cap || count > c->cap - first) return CRDT_E_INVALID;
     if (count == 0) return CRDT_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(c->table + first, 0x80, count * sizeof(Row), c->stream));
+    HIPCHK(hipMemsetAsync(c->table.hot + first, 0x80, count * sizeof(Row), c->stream));
+    HIPCHK(hipMemsetAsync(c->table.cold + first, 0x80, count * sizeof(RowX), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
 }
@@ -2208,7 +2225,7 @@ int crdt_remap_ranks(crdt_ctx* c, uint64_t n_rows, const uint32_t* old_to_new, u
     const uint32_t* dl;
     int st;
     if ((st = stage(c, c->s_rank, old_to_new, n_ranks, CRDT_MEM_HOST, &dl))) return st;
-    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table, n_rows, dl, n_ranks);
+    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table.hot, n_rows, dl, n_ranks);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
