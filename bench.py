@@ -66,11 +66,19 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
     p.add_argument("--exact-counts", action="store_true",
                    help="per-record n_present / n_won also on the sorted path (its changeset-ordered form)")
+    p.add_argument("--ab", default=None, metavar="VAR=v1,v2",
+                   help="development A/B: the timed steps alternate the library switch VAR over the values "
+                        "(one process, one memory placement); per-value step times go to stderr")
     return p.parse_args()
 
 
 def main():
     args = parse()
+    ab = None
+    if args.ab:
+        var, vals = args.ab.split("=", 1)
+        ab = (var, vals.split(","), {})
+        os.environ["CRDT_ENV_DYNAMIC"] = "1"        # the library re-reads its switches per merge
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -200,13 +208,17 @@ def main():
         step_ms, tsum, res = [], {}, None
         table.set_timing(True)
         table_timing[0] = True
-        for _ in range(steps):
+        for si in range(steps):
+            if ab:
+                os.environ[ab[0]] = ab[1][si % len(ab[1])]
             reset()
             barrier()
             ts = time.perf_counter()
             res = step()
             barrier()
             step_ms.append(all_max(time.perf_counter() - ts) * 1e3)       # max over ranks
+            if ab:
+                ab[2].setdefault(ab[1][si % len(ab[1])], []).append(step_ms[-1])
             tms, table_timing[1] = table_timing[1] or [table.timing()], []
             tm = {k: sum(t[k] for t in tms) for k in tms[0]}
             if wl.get("per_call"):                   # sampled calls -> per-step estimates
@@ -224,6 +236,11 @@ def main():
         reset()
         step()
     step_ms, tsum, res = timed_run(args.steps)
+    if ab:
+        for v, ms in ab[2].items():
+            log(f"A/B {ab[0]}={v}: mean {np.mean(ms):.3f} ms  min {np.min(ms):.3f}  max {np.max(ms):.3f}  "
+                f"({len(ms)} steps)")
+        os.environ.pop(ab[0], None)
     assert res["status"] == 0, res
     ms_per_step = float(np.mean(step_ms))
     total_records = wl["total"]

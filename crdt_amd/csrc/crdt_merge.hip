@@ -1132,6 +1132,7 @@ struct crdt_ctx {
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
     uint32_t exp = 0;
+    bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
     bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
@@ -1812,9 +1813,14 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 c->d_misc, c->exp);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
-            k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
-                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
-                c->d_misc, c->exp);
+            if (c->exp & 64u)
+                k_resolve_packed<false, false><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, c->exp);
+            else
+                k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, c->exp);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -1938,6 +1944,16 @@ int crdt_device_count(int* out) {
     return CRDT_OK;
 }
 
+// Tuning switches; with CRDT_ENV_DYNAMIC=1 re-read at every crdt_merge, so one
+// process can alternate them step by step (A/B runs on one memory placement: tools/ab_steps.sh).
+static void read_env_knobs(crdt_ctx* c) {
+    if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_EXP")) c->exp = (uint32_t)atoi(e);   // timing experiments: wrong results
+}
+
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
     if (!out) return CRDT_E_INVALID;
     *out = nullptr;
@@ -1954,11 +1970,8 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (const char* e = getenv("CRDT_MERGE_PATH")) {
         c->merge_path = strcmp(e, "gather") == 0 ? 1 : strcmp(e, "sorted") == 0 ? 2 : 0;
     }
-    if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_EXP")) c->exp = (uint32_t)atoi(e);   // timing experiments: wrong results
+    read_env_knobs(c);
+    if (const char* e = getenv("CRDT_ENV_DYNAMIC")) c->env_dynamic = atoi(e) != 0;
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
@@ -2245,6 +2258,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         return CRDT_OK;
     }
     HIPCHK(hipSetDevice(c->device));
+    if (c->env_dynamic) read_env_knobs(c);
     if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
     // Host batches are staged once; every phase then sees device columns.
     crdt_batch dev = *batch;
