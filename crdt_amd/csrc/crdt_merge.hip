@@ -1144,6 +1144,7 @@ struct crdt_ctx {
     const uint32_t* hist1_key = nullptr;
     uint32_t hist1_shift = 0;
     bool last_packed = false;       // the last sorted apply used the packed form
+    bool last_key8 = false;         // ... with 1-B final key columns
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
     Segs segs;                      // changeset segments of the columns the apply phase reads
@@ -1663,6 +1664,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     }
     c->last_packed = pk;
     c->last_hist1_fused = false;
+    // final records with a 1-B key column when the packed key leaves 4 bits free (two levels)
+    const bool k8 = pk && two && pf.key4 && !(c->exp & 128u);
+    c->last_key8 = k8;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -1771,8 +1775,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
                     c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
             else if (pk)
-                k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                if (k8)
+                    k_part_scatter2<false, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                else
+                    k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
             else
                 k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
                     c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
@@ -1808,13 +1816,22 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
-            k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
-                bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val, pf,
-                c->d_misc, c->exp);
+            if (k8)
+                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, c->exp);
+            else
+                k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, c->exp);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             if (c->exp & 64u)
                 k_resolve_packed<false, false><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, c->exp);
+            else if (k8)
+                k_resolve_packed<false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc, c->exp);
             else
@@ -2344,6 +2361,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_packed) f |= CRDT_PLAN_PACKED;
         if (c->cap > (1ull << 20)) f |= CRDT_PLAN_TWO_LEVEL;
         if (c->last_hist1_fused) f |= CRDT_PLAN_HIST_IN_SCAN;
+        if (c->last_key8) f |= CRDT_PLAN_KEY8;
     }
     *flags = f;
     return CRDT_OK;

@@ -251,7 +251,8 @@ enum crdt_plan_flags {
     CRDT_PLAN_SORTED = 1,        /* the sorted path ran */
     CRDT_PLAN_PACKED = 2,        /* ... in its packed order-free form (64-bit keys, sorted_path.inc) */
     CRDT_PLAN_TWO_LEVEL = 4,     /* ... with two partition levels (capacity > 2^20) */
-    CRDT_PLAN_HIST_IN_SCAN = 8   /* ... with its level-1 histogram counted by the scan */
+    CRDT_PLAN_HIST_IN_SCAN = 8,  /* ... with its level-1 histogram counted by the scan */
+    CRDT_PLAN_KEY8 = 16          /* ... with 13-B final records (1-B key column, 4 key bits in the packed key) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

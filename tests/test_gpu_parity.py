@@ -611,6 +611,7 @@ def test_sorted_hist_in_scan(gpu_device, monkeypatch, kind, cap):
                               device_cols=True)
     assert res["path"] == "sorted" and res["plan"]["hist_in_scan"], res["plan"]
     assert res["plan"]["two_level"] == (cap is not None)
+    assert res["plan"]["key8"] == (cap is not None), res["plan"]      # these frames leave 4 bits free
     if kind == "late_drift":
         assert res["status"] != 0 and res["n_stored"] < len(case["offsets"]) - 1
     monkeypatch.setenv("CRDT_HIST_FUSE", "0")
@@ -658,6 +659,28 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
         assert np.array_equal(a, orows[f]), f
     assert res["canonical_lt"] == ores["canonical_lt"]
     t.close()
+
+
+@pytest.mark.parametrize("L", [42, 43, 44, 45])
+def test_sorted_key8_frame_boundary(gpu_device, L):
+    """The 1-B key column needs 4 free bits above the packed key (L + K + 13 <= 60, L / K the lt /
+    rank field widths): lt spans on both sides of that boundary, stretched downwards by old
+    records (no clock effect) — key8 on / off as the frame says, same rows as the oracle."""
+    case = make_case(seed=98 + L, R=40, per_cs=1500, n_local=2500, n_new=1500, millis_span=4,
+                     counter_span=3, n_ranks=9, tomb_frac=0.1)
+    rng = np.random.default_rng(L)
+    lt = case["lt"].copy()
+    hi = int(lt.max())
+    pick = np.nonzero(rng.random(len(lt)) < 0.02)[0]
+    lt[pick] = hi - rng.integers(0, 1 << (L - 1), len(pick))
+    lt[pick[0]] = hi - ((1 << (L - 1)) + 5)                     # lt span + 1 has exactly L bits
+    case["lt"] = lt
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 17)
+    assert res["path"] == "sorted" and res["plan"]["packed"], res["plan"]
+    span = int(lt.max()) - int(lt.min())
+    assert (span + 1).bit_length() == L
+    K = (int(case["rank"].max()) - int(case["rank"].min()) + 1).bit_length()
+    assert res["plan"]["key8"] == (L + K + 13 <= 60), (L, K, res["plan"])
 
 
 def test_sorted_wide_frame_takes_list_form(gpu_device):
