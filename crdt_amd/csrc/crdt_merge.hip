@@ -1666,6 +1666,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     c->last_hist1_fused = false;
     // final records with a 1-B key column when the packed key leaves 4 bits free (two levels)
     const bool k8 = pk && two && pf.key4 && !(c->exp & 128u);
+    const bool k16 = k8 && !(c->exp & 256u);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
@@ -1741,8 +1742,16 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
-        if (cols.packed_in)
+        if (cols.packed_in && k16)
+            k_part_scatter1<true, true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                c->p1_kj.p, xper1, pf);
+        else if (cols.packed_in)
             k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
+                c->p1_kj.p, xper1, pf);
+        else if (k16)
+            k_part_scatter1<true, false, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
                 c->p1_kj.p, xper1, pf);
         else if (pk)
@@ -1764,8 +1773,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                                             c->p_tseg.p);
             const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
-                                                                  c->p_hist.p);
+            if (k16)   // key bits [4, 20) in 2 B: the level-2 digit (key bits [12, 20)) is its high byte
+                k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap,
+                                                                          kSBits - 4, c->p_hist.p);
+            else
+                k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
+                                                                      c->p_hist.p);
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
             k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
@@ -1775,7 +1788,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
                     c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
             else if (pk)
-                if (k8)
+                if (k16)
+                    k_part_scatter2<false, true, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits - 4, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
                         c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
                 else
