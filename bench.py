@@ -323,8 +323,23 @@ def main():
                 "value": 30.4e9, "unit": "records/s", "achieved": round(rate, 1), "frac": round(rate / 30.4e9, 3),
                 "source": "profiles/r01_ubench_rowwrite.txt"}
     elif path == "sorted" and apply_ms > 0:
-        roofline["dominant_kernel"] = {"kernel": "sorted apply: k_part_* x2 + k_resolve",
-                                       "apply_ms_per_step": round(apply_ms / K, 3)}
+        # the level-1 partition scatter (one launch per step, HIP events around it): reads every
+        # applied record's 20 B, writes its partition record (packed 12 B + key column, or 16 + 4 B)
+        plan = table.last_plan()
+        out_b = (12 + 2) if plan["key16"] else (12 + 4) if plan["packed"] else (16 + 4)
+        p1_us = tsum.get("part1_ms", 0.0) * 1e3 / K
+        n_app = int(offs[-1]) if world == 1 else None
+        dk = {"kernel": "k_part_scatter1 (level-1 partition, one launch per step)",
+              "phases_ms_per_step": {k: round(tsum.get(f"{k}_ms", 0.0) / K, 3)
+                                     for k in ("scan", "part1", "part2", "resolve")},
+              "apply_ms_per_step": round(apply_ms / K, 3), "plan": plan}
+        if p1_us > 0 and n_app:
+            kb = n_app * (20 + out_b)
+            dk.update({"avg_launch_us": round(p1_us, 1), "alg_bytes_per_launch": kb,
+                       "bytes_per_record": f"20 read + {out_b} written",
+                       "achieved_GBs": round(kb / (p1_us / 1e6) / 1e9, 1),
+                       "frac": round(kb / (p1_us / 1e6) / HBM_PEAK, 4)})
+        roofline["dominant_kernel"] = dk
     # traffic: HBM bytes per step from this round's rocprofv3 --pmc passes of this exact command
     if os.path.exists(PMC_FILE) and args.config == "fanin" and world == 1:
         try:

@@ -49,7 +49,8 @@ class CrdtTiming(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("clock_ms", ctypes.c_double),
                 ("apply_ms", ctypes.c_double), ("apply_launches", ctypes.c_uint32),
                 ("apply_total", ctypes.c_uint32), ("total_ms", ctypes.c_double),
-                ("route_ms", ctypes.c_double)]
+                ("route_ms", ctypes.c_double), ("part1_ms", ctypes.c_double), ("part2_ms", ctypes.c_double),
+                ("resolve_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

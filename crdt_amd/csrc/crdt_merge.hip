@@ -1068,6 +1068,12 @@ struct Segs {
 
 }  // namespace
 
+// CRDT_SORTED_FORM bits: switch off a refinement of the packed sorted form (same results; the
+// in-process A/B runs of DESIGN.md §5.2 measure each one against the form without it)
+constexpr uint32_t kFormNoWholeLines = 64;   // resolve writes changed rows only (partial lines)
+constexpr uint32_t kFormNoKey8 = 128;        // 16-B final records (4-B key column)
+constexpr uint32_t kFormNoKey16 = 256;       // 16-B level-1 records (4-B key column)
+
 struct crdt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1111,6 +1117,7 @@ struct crdt_ctx {
     bool timing = false;
     std::vector<hipEvent_t> events;
     std::vector<uint32_t> windows;  // launches of each timed apply window (events ev_window(k, *))
+    bool sorted_phases = false;     // events ev_window(1..3, *) bracket the sorted path's phases
     uint32_t apply_total = 0;
     // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
     int merge_path = 0;
@@ -1131,7 +1138,7 @@ struct crdt_ctx {
     bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
-    uint32_t exp = 0;
+    uint32_t form_off = 0;          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
     bool last_hist1_fused = false;
@@ -1145,6 +1152,7 @@ struct crdt_ctx {
     uint32_t hist1_shift = 0;
     bool last_packed = false;       // the last sorted apply used the packed form
     bool last_key8 = false;         // ... with 1-B final key columns
+    bool last_key16 = false;        // ... and 2-B level-1 key columns
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
     Segs segs;                      // changeset segments of the columns the apply phase reads
@@ -1291,7 +1299,9 @@ int reset_misc(crdt_ctx* c) {
 // apply start (route_ms = the gap before it), end; then one pair per sampled apply window.
 constexpr size_t kEvStart = 0, kEvScan = 1, kEvClock = 2, kEvApply = 3, kEvEnd = 4;
 inline size_t ev_window(size_t k, bool end) { return 5 + 2 * k + (end ? 1 : 0); }
-inline size_t events_for(size_t nsegs) { return ev_window(nsegs / kTimingStride + 2, true) + 1; }
+inline size_t events_for(size_t nsegs) {     // (windows 1..3 also bracket the sorted path's phases)
+    return std::max(ev_window(nsegs / kTimingStride + 2, true), ev_window(3, true)) + 1;
+}
 
 inline void ev_record(crdt_ctx* c, size_t idx) {
     if (c->timing && idx < c->events.size()) hipEventRecord(c->events[idx], c->stream);
@@ -1664,10 +1674,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     }
     c->last_packed = pk;
     c->last_hist1_fused = false;
+    c->sorted_phases = false;
     // final records with a 1-B key column when the packed key leaves 4 bits free (two levels)
-    const bool k8 = pk && two && pf.key4 && !(c->exp & 128u);
-    const bool k16 = k8 && !(c->exp & 256u);     // ... and 2-B level-1 key columns
+    const bool k8 = pk && two && pf.key4 && !(c->form_off & kFormNoKey8);
+    const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
+    c->last_key16 = k16;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -1741,6 +1753,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
+        const bool ph = c->timing && s0 == 0;       // phase events: the first window
+        if (ph) ev_record(c, ev_window(1, false));
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         if (cols.packed_in && k16)
             k_part_scatter1<true, true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
@@ -1762,6 +1776,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_part_scatter1<false><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
                 c->p1_kj.p, xper1, pf);
+        if (ph) ev_record(c, ev_window(1, true));
+        if (ph) ev_record(c, ev_window(2, false));
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
@@ -1801,6 +1817,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
                     c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
         }
+        if (ph) ev_record(c, ev_window(2, true));
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
         const uint32_t nb = two ? kDigits * kDigits : kDigits;
         const uint32_t* bst = two ? c->p_dstart2.p : c->p_dstart1.p;
@@ -1818,6 +1835,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         KeyState ps{c->p_kslt.p, c->p_ksu32.p, c->p_ksu32.p + ksn, c->p_ksu32.p + 2 * ksn};
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
+        if (ph) ev_record(c, ev_window(3, false));
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
@@ -1835,25 +1853,25 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, c->exp);
+                    pf, c->d_misc);
             else
                 k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, c->exp);
+                    pf, c->d_misc);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
-            if (c->exp & 64u)
+            if (c->form_off & kFormNoWholeLines)
                 k_resolve_packed<false, false><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, c->exp);
+                    pf, c->d_misc);
             else if (k8)
                 k_resolve_packed<false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, c->exp);
+                    pf, c->d_misc);
             else
                 k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, c->exp);
+                    pf, c->d_misc);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -1863,6 +1881,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_resolve<false, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                            rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
                                                                            c->d_misc);
+        }
+        if (ph) {
+            ev_record(c, ev_window(3, true));
+            c->sorted_phases = true;
         }
         HIPCHK(hipGetLastError());
     }
@@ -1940,6 +1962,11 @@ void collect_timing(crdt_ctx* c) {
         }
         t.apply_total = c->apply_total;
         t.total_ms = el(kEvStart, kEvEnd);
+        if (c->last_sorted && c->sorted_phases) {
+            t.part1_ms = el(ev_window(1, false), ev_window(1, true));
+            t.part2_ms = el(ev_window(2, false), ev_window(2, true));
+            t.resolve_ms = el(ev_window(3, false), ev_window(3, true));
+        }
     }
     c->last_timing = t;
 }
@@ -1984,7 +2011,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_EXP")) c->exp = (uint32_t)atoi(e);   // timing experiments: wrong results
+    if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
 }
 
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
@@ -2378,6 +2405,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->cap > (1ull << 20)) f |= CRDT_PLAN_TWO_LEVEL;
         if (c->last_hist1_fused) f |= CRDT_PLAN_HIST_IN_SCAN;
         if (c->last_key8) f |= CRDT_PLAN_KEY8;
+        if (c->last_key16) f |= CRDT_PLAN_KEY16;
     }
     *flags = f;
     return CRDT_OK;

@@ -287,7 +287,7 @@ class DeviceTable:
         self._check(self._lib.crdt_last_path(self._ctx, ctypes.byref(v)), "crdt_last_path")
         return {1: "gather", 2: "sorted"}[v.value]
 
-    PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16}
+    PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32}
 
     def last_plan(self) -> dict:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""

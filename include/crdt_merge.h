@@ -102,6 +102,11 @@ typedef struct crdt_timing {
     uint32_t apply_total;      /* apply launches in the call */
     double total_ms;           /* first to last event of the call */
     double route_ms;           /* sharded ctx: route count, count exchange, scatter, record exchange */
+    /* sorted path (first window of changesets): the level-1 partition scatter, the level-2 partition
+       (its histogram and scatter), the resolve (fold, carry and resolve launches); 0 otherwise */
+    double part1_ms;
+    double part2_ms;
+    double resolve_ms;
 } crdt_timing;
 
 /* ---- lifecycle ------------------------------------------------------------ */
@@ -252,7 +257,8 @@ enum crdt_plan_flags {
     CRDT_PLAN_PACKED = 2,        /* ... in its packed order-free form (64-bit keys, sorted_path.inc) */
     CRDT_PLAN_TWO_LEVEL = 4,     /* ... with two partition levels (capacity > 2^20) */
     CRDT_PLAN_HIST_IN_SCAN = 8,  /* ... with its level-1 histogram counted by the scan */
-    CRDT_PLAN_KEY8 = 16          /* ... with 13-B final records (1-B key column, 4 key bits in the packed key) */
+    CRDT_PLAN_KEY8 = 16,         /* ... with 13-B final records (1-B key column, 4 key bits in the packed key) */
+    CRDT_PLAN_KEY16 = 32         /* ... and 14-B level-1 records (2-B key column) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 
