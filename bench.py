@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
     p.add_argument("--exact-counts", action="store_true",
                    help="per-record n_present / n_won also on the sorted path (its changeset-ordered form)")
+    p.add_argument("--late-alloc", action="store_true",
+                   help="create the table after the workload (the library allocates its scratch in the first merge)")
     p.add_argument("--ab", default=None, metavar="VAR=v1,v2",
                    help="development A/B: the timed steps alternate the library switch VAR over the values "
                         "(one process, one memory placement); per-value step times go to stderr")
@@ -113,6 +115,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return int(t.item())
 
+    # the fan-in's table and partition scratch are allocated before the workload, while device
+    # memory is unfragmented (the library's big buffers then sit in few large fragments)
+    table = None
+    if args.config == "fanin" and not args.late_alloc:
+        table = DeviceTable(local_rank, local_rank=0, capacity=-(-args.keys // world))
+        table.reserve_scratch(args.records if world == 1 else int(args.records / world * 1.25))
+        torch.cuda.synchronize()
+
     t0 = time.time()
     census = args.config == "fanin" and not args.no_census and world > 1      # N > 1: counted at generation
     if args.config == "fanin":
@@ -141,7 +151,9 @@ def main():
     torch.cuda.synchronize()
     log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
 
-    table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
+    if table is None:
+        table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
+    assert table.capacity >= wl["capacity"]
     table.set_merge_path(args.path)
     # per-record n_present / n_won are library extras (not reference results); without them the
     # sorted path folds each bucket in any order (same rows / canonical / status)
@@ -236,6 +248,7 @@ def main():
         reset()
         step()
     step_ms, tsum, res = timed_run(args.steps)
+    plan = table.last_plan()                        # (later merges — census, samples — may go elsewhere)
     if ab:
         for v, ms in ab[2].items():
             log(f"A/B {ab[0]}={v}: mean {np.mean(ms):.3f} ms  min {np.min(ms):.3f}  max {np.max(ms):.3f}  "
@@ -325,7 +338,6 @@ def main():
     elif path == "sorted" and apply_ms > 0:
         # the level-1 partition scatter (one launch per step, HIP events around it): reads every
         # applied record's 20 B, writes its partition record (packed 12 B + key column, or 16 + 4 B)
-        plan = table.last_plan()
         out_b = (12 + 2) if plan["key16"] else (12 + 4) if plan["packed"] else (16 + 4)
         p1_us = tsum.get("part1_ms", 0.0) * 1e3 / K
         n_app = int(offs[-1]) if world == 1 else None

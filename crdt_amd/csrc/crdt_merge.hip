@@ -1138,7 +1138,8 @@ struct crdt_ctx {
     bool packed_resolve = true;     // order-free sorted path: packed-key resolve when the frame fits (CRDT_PACKED=0: off)
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
-    uint32_t form_off = 0;          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
+    uint32_t form_off = 0;
+    uint32_t l1_shift_kb = 0, l2_shift_kb = 0;   // CRDT_L1_SHIFT / CRDT_L2_SHIFT (KB, < 4096)          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
     bool last_hist1_fused = false;
@@ -1727,7 +1728,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         HIPALLOC(c->p_part.ensure((size_t)ncm * kDigits));
         HIPALLOC(c->p_choff.ensure((size_t)ncm * kDigits));
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
-        HIPALLOC(c->p1_rec.ensure(nw)); HIPALLOC(c->p1_kj.ensure(nw));
+        // partition buffers, each base shifted by the CRDT_L{1,2}_SHIFT knob (KB; placement A/B runs)
+        constexpr size_t kShiftPad = 4u << 20;                      // bytes
+        HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4));
+        u32x4* p1r = c->p1_rec.p + (size_t)c->l1_shift_kb * 64;
+        uint32_t* p1k = c->p1_kj.p + (size_t)c->l1_shift_kb * 256;
+        u32x4* p2r = nullptr;
+        uint32_t* p2k = nullptr;
         const uint64_t* d_beg = c->p_plan.p;
         const uint64_t* d_end = c->p_plan.p + nseg;
         const uint32_t* d_sj = reinterpret_cast<const uint32_t*>(c->p_plan.p + 2 * (size_t)nseg);
@@ -1758,30 +1765,32 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         if (cols.packed_in && k16)
             k_part_scatter1<true, true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                c->p1_kj.p, xper1, pf);
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf);
         else if (cols.packed_in)
             k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                c->p1_kj.p, xper1, pf);
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf);
         else if (k16)
             k_part_scatter1<true, false, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                c->p1_kj.p, xper1, pf);
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf);
         else if (pk)
             k_part_scatter1<true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                c->p1_kj.p, xper1, pf);
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf);
         else
             k_part_scatter1<false><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, c->p1_rec.p,
-                c->p1_kj.p, xper1, pf);
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf);
         if (ph) ev_record(c, ev_window(1, true));
         if (ph) ev_record(c, ev_window(2, false));
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
-            HIPALLOC(c->p2_rec.ensure(nw)); HIPALLOC(c->p2_kj.ensure(nw));
+            HIPALLOC(c->p2_rec.ensure(nw + kShiftPad / 16)); HIPALLOC(c->p2_kj.ensure(nw + kShiftPad / 4));
+            p2r = c->p2_rec.p + (size_t)c->l2_shift_kb * 64;
+            p2k = c->p2_kj.p + (size_t)c->l2_shift_kb * 256;
             uint32_t* tb2 = c->p_l2map.p;
             uint32_t* cb2 = c->p_l2map.p + kDigits + 1;
             k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2);
@@ -1790,10 +1799,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
             if (k16)   // key bits [4, 20) in 2 B: the level-2 digit (key bits [12, 20)) is its high byte
-                k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap,
+                k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap,
                                                                           kSBits - 4, c->p_hist.p);
             else
-                k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(c->p1_kj.p, tm2, 0, c->d_misc, c->cap, kSBits,
+                k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap, kSBits,
                                                                       c->p_hist.p);
             k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
@@ -1802,27 +1811,27 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint32_t xper2 = c->xcd_map ? (nt2 + kXcds - 1) / kXcds : 0;
             if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
             else if (pk)
                 if (k16)
                     k_part_scatter2<false, true, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits - 4, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2);
                 else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
                 else
                     k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
             else
                 k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    c->p1_rec.p, c->p1_kj.p, tm2, kSBits, c->p_toff.p, c->p2_rec.p, c->p2_kj.p, xper2);
+                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
         }
         if (ph) ev_record(c, ev_window(2, true));
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
         const uint32_t nb = two ? kDigits * kDigits : kDigits;
         const uint32_t* bst = two ? c->p_dstart2.p : c->p_dstart1.p;
-        const u32x4* rec = two ? c->p2_rec.p : c->p1_rec.p;
-        const uint32_t* rv = two ? c->p2_kj.p : c->p1_kj.p;
+        const u32x4* rec = two ? p2r : p1r;
+        const uint32_t* rv = two ? p2k : p1k;
         const uint32_t max_items = nb + (uint32_t)(nw / kRPart) + 1;
         const size_t ksn = (size_t)(2 * (nw / kRPart) + 2) * kSKeys;     // part-state slots of split buckets
         const uint32_t max_hot = std::min<uint32_t>(nb, (uint32_t)(nw / kRPart) + 1);   // split buckets hold > kRPart
@@ -2012,6 +2021,8 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
+    if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
+    if (const char* e = getenv("CRDT_L2_SHIFT")) c->l2_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
 }
 
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
@@ -2113,6 +2124,18 @@ int crdt_reserve(crdt_ctx* c, uint64_t capacity) {
     if (c->table.cold) hipFree(c->table.cold);
     c->table = t;
     c->cap = newcap;
+    return CRDT_OK;
+}
+
+int crdt_reserve_scratch(crdt_ctx* c, uint64_t n_records) {
+    if (!c) return CRDT_E_INVALID;
+    if (n_records == 0) return CRDT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    constexpr size_t kShiftPad = 4u << 20;        // as apply_sorted sizes them
+    HIPALLOC(c->p1_rec.ensure(n_records + kShiftPad / 16));
+    HIPALLOC(c->p1_kj.ensure(n_records + kShiftPad / 4));
+    HIPALLOC(c->p2_rec.ensure(n_records + kShiftPad / 16));
+    HIPALLOC(c->p2_kj.ensure(n_records + kShiftPad / 4));
     return CRDT_OK;
 }
 

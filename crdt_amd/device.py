@@ -273,6 +273,10 @@ class DeviceTable:
         bucket in any order (same rows / canonical / status; both counts reported as 2^64 - 1)."""
         self._check(self._lib.crdt_set_counts(self._ctx, 1 if exact else 0), "crdt_set_counts")
 
+    def reserve_scratch(self, n_records: int):
+        """crdt_reserve_scratch: size the sorted path's partition buffers up front."""
+        self._check(self._lib.crdt_reserve_scratch(self._ctx, int(n_records)), "crdt_reserve_scratch")
+
     def set_rank_bound(self, bound: int):
         """crdt_set_rank_bound: every later rank is < bound (0: no promise).  The sorted path then
         needs no pass over the ranks for its packed key's frame."""

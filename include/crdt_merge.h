@@ -120,6 +120,10 @@ int crdt_device_count(int* out);
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out);
 void crdt_destroy(crdt_ctx* ctx);
 int crdt_reserve(crdt_ctx* ctx, uint64_t capacity);          /* grow; new rows absent */
+/* Pre-size the sorted path's partition scratch for merges of up to n_records applied records
+ * (two partitioned copies, <= 40 B per record), so the first large merge allocates nothing and the
+ * buffers are placed while device memory is still unfragmented.  Optional. */
+int crdt_reserve_scratch(crdt_ctx* ctx, uint64_t n_records);
 int crdt_capacity(const crdt_ctx* ctx, uint64_t* out);
 int crdt_set_local_rank(crdt_ctx* ctx, uint32_t rank);        /* after a rank remap */
 
