@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _capi
 from .crdt_json import CrdtJson
-from .device import DeviceTable
+from .device import CrdtNativeError, DeviceTable
 from .hlc import (ClockDriftException, DuplicateNodeException, Hlc, OverflowException, now_millis)
 from .intern import NULL_HANDLE, KeyIndex, NodeRanks, ValueStore
 from .record import Record
@@ -402,7 +402,15 @@ class MapCrdt(Crdt):
             for x, ms in odd:
                 millis[x] = ms
         self._reserve()
-        res, flags = self._table.merge(kid, lt, rank, val, offsets, wall, millis=millis)
+        try:
+            res, flags = self._table.merge(kid, lt, rank, val, offsets, wall, millis=millis)
+        except CrdtNativeError:
+            # the library refused the call (nothing stored on a single context, include/crdt_merge.h):
+            # forget the keys and value handles this batch interned
+            self._keys.truncate(newid_start[0])
+            for x in range(n_total):
+                self._values.release(int(val[x]))
+            raise
         stop = res["n_stored"]
         # keys first seen in changesets that were not stored never entered the map
         self._keys.truncate(newid_start[stop])

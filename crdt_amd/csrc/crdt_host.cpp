@@ -819,13 +819,26 @@ int decode_parallel(const char* js, uint64_t len, crdt_keys* keys, crdt_decoded*
     }
     // phase 2: chunks in order while each one's parse was valid and ended where the next began
     Builder bld(keys, d);
-    uint64_t total = 0, kbytes = 0;
-    for (const auto& c : ch) { total += c.kid.size(); kbytes += c.karena.size(); }
-    keys->reserve(total, kbytes);
+    // the key table grows by at most the phase-1 misses (records whose key it did not hold):
+    // reserve and prefault that much only, so a re-sync of known keys leaves it as it was; the
+    // per-call columns are reserved (and prefaulted) for every record and freed after the call
+    uint64_t total = 0, miss = 0, mbytes = 0;
+    for (const auto& c : ch) {
+        total += c.kid.size();
+        for (size_t m = 0; m < c.kid.size(); ++m)
+            if (c.kid[m] == UINT32_MAX) { ++miss; mbytes += c.klen[m]; }
+    }
+    keys->reserve(miss, mbytes);
     d->key.reserve(total); d->lt.reserve(total); d->node.reserve(total); d->voff.reserve(total); d->vlen.reserve(total);
-    bld.first_new.reserve(total);
-    prefault({spare(d->key), spare(d->lt), spare(d->node), spare(d->voff), spare(d->vlen), spare(bld.first_new),
-              spare(keys->arena), spare(keys->off), spare(keys->hash)});
+    bld.first_new.reserve(miss);
+    std::vector<Span> spans{spare(d->key), spare(d->lt), spare(d->node), spare(d->voff), spare(d->vlen),
+                            spare(bld.first_new)};
+    if (miss) {                                           // (the table's spare beyond the misses stays virtual)
+        spans.push_back(spare(keys->arena));
+        spans.push_back(spare(keys->off));
+        spans.push_back(spare(keys->hash));
+    }
+    prefault(spans);
     uint64_t resume = 0;                                  // != 0: decode sequentially from here
     bool closed = false;
     std::vector<uint32_t> nmap;

@@ -626,7 +626,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     uint64_t end, uint32_t j, Table table, uint64_t cap,
     const int64_t* __restrict__ Rj, Misc* __restrict__ misc, uint8_t* __restrict__ flags)
 {
-    if (j >= misc->stop) return;                          // uniform: changeset past the stop point
+    if (j >= misc->stop || (misc->err & 1u)) return;      // uniform: past the stop point / a bad key id
     const int64_t stamp = Rj[j];
     // striped: record q of this thread = base + q * 256 + tid, so a wave's q-th
     // access covers 64 consecutive records (coalesced streams; consecutive new ids
@@ -859,6 +859,17 @@ __global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long l
     out[1] = (long long)nw;
     out[2] = misc->err ? 1 : 0;
     out[3] = counted ? 0 : 1;
+}
+
+// Key ids against the capacity before any row is stored (resident batches of the gather path;
+// the sorted path checks them in its level-1 scatter, before its resolve stores anything).
+__global__ __launch_bounds__(256) void k_key_check(const uint32_t* __restrict__ key, uint64_t n, uint64_t cap,
+                                                   Misc* __restrict__ misc)
+{
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        bad |= __builtin_nontemporal_load(key + i) >= cap;
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
 }
 
 // ----------------------------------------------------------------- SPI kernels
@@ -1154,6 +1165,7 @@ struct crdt_ctx {
     bool last_packed = false;       // the last sorted apply used the packed form
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
+    bool keys_checked = false;      // the gather apply checked every key id before storing
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
     Segs segs;                      // changeset segments of the columns the apply phase reads
@@ -1527,7 +1539,14 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
         if (out) *out = res;
         return res.status;
     }
-    if (err) res.status = CRDT_E_KEY_RANGE;
+    if (err) {
+        res.status = CRDT_E_KEY_RANGE;
+        if ((sorted || c->keys_checked) && (c->h_misc->err & 1u)) {   // this ctx stored nothing
+            res.canonical_lt = c->canonical;
+            if (out) *out = res;
+            return res.status;
+        }
+    }
     c->canonical = res.canonical_lt;
     if (out) *out = res;
     return res.status;
@@ -1551,6 +1570,12 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const Segs& sg, uint64_t n, int3
     if (!c->resolved)
         k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     c->resolved = false;
+    // resident keys are checked up front, so a bad id stores nothing (host batches stream their
+    // keys in under K2: there the K2 launches after the first bad id store nothing)
+    c->keys_checked = !c->kv_key;
+    if (c->keys_checked && n)
+        k_key_check<<<std::min<uint32_t>(grid_for(n, 256 * 16), 4096), 256, 0, c->stream>>>(cols.key, n, c->cap,
+                                                                                           c->d_misc);
     ev_record(c, kEvApply);
     c->windows.clear();
     uint32_t nl = 0;
@@ -1852,7 +1877,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                     c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
             k_part_carry<false><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table,
-                                                                                    c->cap, ps, cy, c->d_Rj.p, jb);
+                                                                                    c->cap, ps, cy, c->d_Rj.p, jb, c->d_misc);
             k_resolve<false><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                      c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
         } else if (pk) {   // packed order-free form: one LDS 64-bit max per record (sorted_path.inc)
@@ -1886,7 +1911,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
                                                                           c->d_misc);
             k_part_carry<true><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table,
-                                                                                   c->cap, ps, cy, c->d_Rj.p, jb);
+                                                                                   c->cap, ps, cy, c->d_Rj.p, jb, c->d_misc);
             k_resolve<false, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                            rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
                                                                            c->d_misc);

@@ -108,6 +108,7 @@ class CrdtLib {
         merge = lib.lookupFunction<_MergeC, _MergeD>('crdt_merge'),
         setMergePath = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_merge_path'),
         setCounts = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_counts'),
+        setRankBound = lib.lookupFunction<_CtxU32C, _CtxIntD>('crdt_set_rank_bound'),
         statusString = lib.lookupFunction<_StatusStrC, _StatusStrD>('crdt_status_string');
 
   factory CrdtLib.open([String path = 'libcrdt_mi355x.so']) => CrdtLib(DynamicLibrary.open(path));
@@ -129,5 +130,6 @@ class CrdtLib {
   final _MergeD merge;
   final _CtxIntD setMergePath;
   final _CtxIntD setCounts;
+  final _CtxIntD setRankBound;
   final _StatusStrD statusString;
 }

@@ -117,6 +117,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
       try {
         _check(_lib.create(_device, _nodes.rank(nodeId), _initialCapacity, out), 'crdt_create');
         _ctx = out.value;
+        _check(_lib.setRankBound(_ctx, _nodes.sorted.length), 'crdt_set_rank_bound');
       } finally {
         calloc.free(out);
       }
@@ -149,7 +150,10 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
 
   void _registerNodes(Iterable<dynamic> nodes) {
     final c = _c;
+    final before = _nodes.sorted.length;
     final lut = _nodes.register(nodes);
+    // ranks are dense (0 .. nodes - 1): the bound lets the sorted path skip reading ranks
+    if (_nodes.sorted.length != before) _check(_lib.setRankBound(c, _nodes.sorted.length), 'crdt_set_rank_bound');
     if (lut == null) return;
     final p = calloc<Uint32>(lut.length);
     try {

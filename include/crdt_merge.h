@@ -50,7 +50,11 @@ enum crdt_status {
     CRDT_E_INVALID = -1,       /* bad argument (offsets, sizes, null pointers) */
     CRDT_E_HIP = -2,           /* HIP runtime error */
     CRDT_E_NOMEM = -3,         /* device allocation failed */
-    CRDT_E_KEY_RANGE = -4,     /* a key_id >= capacity: state after the call is unspecified */
+    CRDT_E_KEY_RANGE = -4,     /* a key_id >= capacity.  crdt_merge on one context: nothing stored and
+                                  the canonical unchanged for device batches and on the sorted path;
+                                  a host batch on the gather path (its keys stream in under the
+                                  apply) may have stored the changesets before the bad id's launch;
+                                  on a sharded context the other ranks' rows are stored */
     CRDT_E_NO_DEVICE = -5,     /* no usable gfx950 device */
     CRDT_E_COMM = -6           /* the communicator failed (RCCL error, missing librccl, a callback's error) */
 };

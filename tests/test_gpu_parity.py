@@ -718,6 +718,38 @@ def test_sorted_split_hot_bucket_packed(gpu_device, monkeypatch, packed):
     assert res["path"] == "sorted"
 
 
+@pytest.mark.parametrize("path", ["gather", "sorted"])
+def test_key_out_of_range_stores_nothing(gpu_device, path):
+    """A key id >= capacity in a device batch: CRDT_E_KEY_RANGE with no row stored and the
+    canonical unchanged, on both store paths (the gather path checks ids before K2, the sorted
+    path's resolve skips once its level-1 scatter saw one)."""
+    import torch
+    from crdt_amd import CrdtNativeError, DeviceTable
+    case = make_case(seed=77, R=70, per_cs=1500, n_local=3000, n_new=1000, millis_span=4, counter_span=2,
+                     n_ranks=5, tomb_frac=0.1)
+    key = case["key"].copy()
+    key[len(key) // 2] = case["n_ids"] + 5                      # capacity is n_ids
+    t = DeviceTable(0, local_rank=case["local_rank"], capacity=case["n_ids"])
+    t.set_merge_path(path)
+    if path == "sorted":
+        t.set_counts(False)
+    loc = case["local"]
+    keep = loc["mod"] != ABSENT_MOD
+    ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
+    t.put_rows(ids, loc["lt"][keep], loc["rank"][keep], loc["val"][keep], loc["mod"][keep])
+    t.canonical = case["c0"]
+    before = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
+    cols = [torch.from_numpy(c).cuda() for c in (key, case["lt"], case["rank"], case["val"])]
+    with pytest.raises(CrdtNativeError, match="key id out of range"):
+        t.merge(*cols, case["offsets"], case["wall"], win_flags=False)
+    assert t.last_path() == path
+    after = t.read_rows(np.arange(case["n_ids"], dtype=np.uint32))
+    for a, b in zip(before, after):
+        assert np.array_equal(a, b)
+    assert t.canonical == case["c0"]
+    t.close()
+
+
 def test_sorted_key_out_of_range(gpu_device):
     from crdt_amd import CrdtNativeError, DeviceTable
     t = DeviceTable(0, local_rank=0, capacity=64)
