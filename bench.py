@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
     p.add_argument("--exact-counts", action="store_true",
                    help="per-record n_present / n_won also on the sorted path (its changeset-ordered form)")
+    p.add_argument("--row-bytes", type=int, choices=[0, 24, 32], default=0,
+                   help="device row size (crdt_set_row_bytes); 0: 32 for the gather-path streaming configs "
+                        "(cfg2, cfg5: random winner writes), else 24")
     p.add_argument("--late-alloc", action="store_true",
                    help="create the table after the workload (the library allocates its scratch in the first merge)")
     p.add_argument("--ab", default=None, metavar="VAR=v1,v2",
@@ -154,6 +157,8 @@ def main():
     if table is None:
         table = DeviceTable(local_rank, local_rank=0, capacity=wl["capacity"])
     assert table.capacity >= wl["capacity"]
+    row_bytes = args.row_bytes or (32 if args.config in ("cfg2", "cfg5") else 24)
+    table.set_row_bytes(row_bytes)
     table.set_merge_path(args.path)
     # per-record n_present / n_won are library extras (not reference results); without them the
     # sorted path folds each bucket in any order (same rows / canonical / status)
@@ -405,6 +410,7 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
         "config": {"workload": workload, "records": total_records, "replicas": R,
                    "parallelism": f"keyshard{n}-routed" if world > 1 else "single", "merge_path": path,
+                   "row_bytes": row_bytes,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp, "parity": parity,
         "pcie_inclusive": pcie, "presharded": presharded,

@@ -112,6 +112,7 @@ SIGNATURES = {
     "crdt_set_counts": (_INT, [_P, _INT]),
     "crdt_set_rank_bound": (_INT, [_P, _U32]),
     "crdt_reserve_scratch": (_INT, [_P, _U64]),
+    "crdt_set_row_bytes": (_INT, [_P, _U32]),
     "crdt_last_plan": (_INT, [_P, _P]),
     "crdt_last_path": (_INT, [_P, _P]),
     "crdt_set_timing": (_INT, [_P, _INT]),

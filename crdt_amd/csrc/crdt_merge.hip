@@ -57,45 +57,60 @@ constexpr int64_t kLowBits = 40;
 constexpr int64_t kLowMask = (1ll << kLowBits) - 1;
 constexpr int64_t kEvNone = INT64_MAX;
 
-// One device row per key id, split by use into two arrays (structure of arrays):
-//   hot  Row  16 B, 16-B aligned — everything the merge decision reads, so the gather of a row
-//             is ONE dwordx4 (random row accesses are request-rate bound: tools/ubench_gather.hip)
-//             and the sorted path's per-bucket row load reads 64 KB per 4096 keys, all of it used:
-//     [0:8)  lt      Record.hlc.logicalTime
-//     [8:12) rank    Record.hlc.nodeId rank
-//     [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the
-//                    visibility test (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
-//   cold RowX  8 B — written with a winning record, read only by the views:
-//     [0:4)  mod_lo  low word of modified
-//     [4:8)  val     Record.value handle
-// (One 32-B row made every bucket load fetch the whole line for its first 16 B and every write
-// cost 32 B: the split takes 8 GB -> 4 GB of row reads and 5.4 -> 4.1 GB of row writes off a
-// 1B-record fan-in over 2^28 keys.)
-struct alignas(16) Row {
-    int64_t lt;
-    uint32_t rank;
-    int32_t mod_hi;
-};
-struct alignas(8) RowX {
-    uint32_t mod_lo;
-    uint32_t val;
-};
-static_assert(sizeof(Row) == 16 && sizeof(RowX) == 8, "row layout");
+// One device row per key id; rows are 24 or 32 B apart (crdt_set_row_bytes), fields in order:
+//   [0:8)  lt      Record.hlc.logicalTime
+//   [8:12) rank    Record.hlc.nodeId rank
+//   [12:16) mod_hi high word of Record.modified.logicalTime; its sign bit is the visibility test
+//                  (mod < 0: invisible to merge / recordMap, map_crdt.dart:42-45)
+//   [16:20) mod_lo low word of modified
+//   [20:24) val    Record.value handle
+//   [24:32) zero   (32-B rows only)
+// The first 16 B are everything the merge decision reads, so a gather of a row is ONE dwordx4
+// (gfx950 loads / stores vectors at any dword alignment).  24-B rows (the default) make every
+// coalesced pass over the table — the sorted path's bucket loads and whole-line writes — move 25 %
+// fewer bytes than 32-B ones; 32-B rows make a random winner write one aligned 32-B store, which the
+// gather path's streaming workloads (most records win) run faster.
 struct Table {
-    Row* hot;
-    RowX* cold;
+    char* base;
+    uint32_t stride;                 // 24 or 32
 };
 
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x8a __attribute__((ext_vector_type(8), aligned(32)));
+
+__host__ __device__ inline char* row_ptr(const Table& t, uint64_t k) { return t.base + k * (uint64_t)t.stride; }
+// the decision half {lt lo, lt hi, rank, mod_hi} of row k / the rest {mod_lo, val}
+__device__ inline uint4 load_hot(const Table& t, uint64_t k) {
+    const u32x4u v = *reinterpret_cast<const u32x4u*>(row_ptr(t, k));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ inline uint2 load_cold(const Table& t, uint64_t k) {
+    const u32x2u v = *reinterpret_cast<const u32x2u*>(row_ptr(t, k) + 16);
+    return make_uint2(v.x, v.y);
+}
+__device__ inline void store_hc(const Table& t, uint64_t k, uint4 h, uint2 x) {
+    char* p = row_ptr(t, k);
+    if (t.stride == 32) {                         // one aligned 32-B store
+        u32x8a a;
+        a.s0 = h.x; a.s1 = h.y; a.s2 = h.z; a.s3 = h.w; a.s4 = x.x; a.s5 = x.y; a.s6 = 0u; a.s7 = 0u;
+        *reinterpret_cast<u32x8a*>(p) = a;
+        return;
+    }
+    u32x4u a;
+    a.x = h.x; a.y = h.y; a.z = h.z; a.w = h.w;
+    *reinterpret_cast<u32x4u*>(p) = a;
+    u32x2u b;
+    b.x = x.x; b.y = x.y;
+    *reinterpret_cast<u32x2u*>(p + 16) = b;
+}
 __device__ inline int64_t row_mod(const Table& t, uint64_t k) {
-    return (int64_t)(((uint64_t)(uint32_t)t.hot[k].mod_hi << 32) | t.cold[k].mod_lo);
+    const uint4 h = load_hot(t, k);
+    return (int64_t)(((uint64_t)h.w << 32) | load_cold(t, k).x);
 }
 __device__ inline void store_row(const Table& t, uint64_t k, int64_t lt, uint32_t rank, uint32_t val, int64_t mod) {
-    uint4 h;                       // one dwordx4 + one dwordx2
-    h.x = (uint32_t)lt; h.y = (uint32_t)((uint64_t)lt >> 32); h.z = rank; h.w = (uint32_t)((uint64_t)mod >> 32);
-    *reinterpret_cast<uint4*>(t.hot + k) = h;
-    uint2 x;
-    x.x = (uint32_t)mod; x.y = val;
-    *reinterpret_cast<uint2*>(t.cold + k) = x;
+    store_hc(t, k, make_uint4((uint32_t)lt, (uint32_t)((uint64_t)lt >> 32), rank, (uint32_t)((uint64_t)mod >> 32)),
+             make_uint2((uint32_t)mod, val));
 }
 
 // Device-side per-call words.
@@ -651,7 +666,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(
     for (int q = 0; q < kApplyItems; ++q) {              // all gathers in flight, one dwordx4 each
         ok[q] = in[q] && k[q] < cap;
         const uint64_t row = ok[q] ? k[q] : 0;
-        h[q] = *reinterpret_cast<const uint4*>(table.hot + row);
+        h[q] = load_hot(table, row);
     }
     int npres = 0, nwon = 0;
     bool bad = false;
@@ -872,6 +887,13 @@ __global__ __launch_bounds__(256) void k_key_check(const uint32_t* __restrict__ 
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
 }
 
+// Copy every row into a table of another row size (crdt_set_row_bytes).
+__global__ __launch_bounds__(256) void k_relayout(Table src, Table dst, uint64_t n)
+{
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256)
+        store_hc(dst, k, load_hot(src, k), load_cold(src, k));
+}
+
 // ----------------------------------------------------------------- SPI kernels
 __global__ __launch_bounds__(256) void k_put_rows(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
@@ -906,23 +928,24 @@ __global__ __launch_bounds__(256) void k_read_rows(
     if (i >= n) return;
     const uint32_t k = key[i];
     if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    const Row row = table.hot[k];
-    if (lt) lt[i] = row.lt;
-    if (rank) rank[i] = row.rank;
-    if (val) val[i] = table.cold[k].val;
-    if (mod) mod[i] = row_mod(table, k);
+    const uint4 h = load_hot(table, k);
+    const uint2 x = load_cold(table, k);
+    if (lt) lt[i] = (int64_t)(((uint64_t)h.y << 32) | h.x);
+    if (rank) rank[i] = h.z;
+    if (val) val[i] = x.y;
+    if (mod) mod[i] = (int64_t)(((uint64_t)h.w << 32) | x.x);
 }
 
 // refreshCanonicalTime (crdt.dart:114-121): max lt over rows visible to recordMap().
-__global__ __launch_bounds__(256) void k_refresh(const Row* __restrict__ table, uint64_t n,
+__global__ __launch_bounds__(256) void k_refresh(Table table, uint64_t n,
                                                  long long* __restrict__ out)
 {
     __shared__ int64_t s[4];
     int64_t m = INT64_MIN;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const Row row = table[i];
-        if (row.mod_hi >= 0) m = imax(m, row.lt);
+        const uint4 h = load_hot(table, i);
+        if ((int32_t)h.w >= 0) m = imax(m, (int64_t)(((uint64_t)h.y << 32) | h.x));
     }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = m;
@@ -1025,13 +1048,14 @@ __global__ void k_event_init(long long* __restrict__ event)
     if (threadIdx.x == 0) { event[0] = kEvNone; event[1] = INT64_MIN; event[2] = 0; event[3] = INT64_MIN; }
 }
 
-__global__ __launch_bounds__(256) void k_remap(Row* __restrict__ table, uint64_t n,
+__global__ __launch_bounds__(256) void k_remap(Table table, uint64_t n,
                                                const uint32_t* __restrict__ lut, uint32_t nl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t r = table[i].rank;
-    if (r < nl) table[i].rank = lut[r];
+    uint32_t* rk = reinterpret_cast<uint32_t*>(row_ptr(table, i) + 8);
+    const uint32_t r = *rk;
+    if (r < nl) *rk = lut[r];
 }
 
 // ============================================================ host-side context
@@ -1089,7 +1113,7 @@ struct crdt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t local_rank = 0;
-    Table table{nullptr, nullptr};  // hot / cold row arrays, capacity rows each
+    Table table{nullptr, 24};       // capacity rows (crdt_set_row_bytes)
     uint64_t cap = 0;
     int64_t canonical = 0;
 
@@ -2099,8 +2123,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
     c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release();
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
-    if (c->table.hot) hipFree(c->table.hot);
-    if (c->table.cold) hipFree(c->table.cold);
+    if (c->table.base) hipFree(c->table.base);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
     c->d_M.release(); c->d_event.release(); c->d_plan.release();
@@ -2127,28 +2150,37 @@ void crdt_destroy(crdt_ctx* c) {
 
 int crdt_reserve(crdt_ctx* c, uint64_t capacity) {
     if (!c) return CRDT_E_INVALID;
-    if (capacity <= c->cap && c->table.hot) return CRDT_OK;
+    if (capacity <= c->cap && c->table.base) return CRDT_OK;
     if (capacity > (1ull << 32)) return CRDT_E_INVALID;   // key ids are uint32
     HIPCHK(hipSetDevice(c->device));
     const uint64_t newcap = std::max<uint64_t>(capacity, 16);
-    Table t{nullptr, nullptr};
-    HIPALLOC(hipMalloc(&t.hot, newcap * sizeof(Row)));
-    if (hipMalloc(&t.cold, newcap * sizeof(RowX)) != hipSuccess) {
-        hipFree(t.hot);
-        return CRDT_E_NOMEM;
-    }
-    if (c->table.hot && c->cap) {
-        HIPCHK(hipMemcpyAsync(t.hot, c->table.hot, c->cap * sizeof(Row), hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(t.cold, c->table.cold, c->cap * sizeof(RowX), hipMemcpyDeviceToDevice, c->stream));
-    }
+    const uint64_t rb = c->table.stride;
+    Table t{nullptr, c->table.stride};
+    HIPALLOC(hipMalloc(&t.base, newcap * rb));
+    if (c->table.base && c->cap)
+        HIPCHK(hipMemcpyAsync(t.base, c->table.base, c->cap * rb, hipMemcpyDeviceToDevice, c->stream));
     // absent rows: mod_hi 0x80808080 < 0 (and mod = 0x8080808080808080)
-    HIPCHK(hipMemsetAsync(t.hot + c->cap, 0x80, (newcap - c->cap) * sizeof(Row), c->stream));
-    HIPCHK(hipMemsetAsync(t.cold + c->cap, 0x80, (newcap - c->cap) * sizeof(RowX), c->stream));
+    HIPCHK(hipMemsetAsync(t.base + c->cap * rb, 0x80, (newcap - c->cap) * rb, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->table.hot) hipFree(c->table.hot);
-    if (c->table.cold) hipFree(c->table.cold);
+    if (c->table.base) hipFree(c->table.base);
     c->table = t;
     c->cap = newcap;
+    return CRDT_OK;
+}
+
+int crdt_set_row_bytes(crdt_ctx* c, uint32_t row_bytes) {
+    if (!c || (row_bytes != 24 && row_bytes != 32)) return CRDT_E_INVALID;
+    if (row_bytes == c->table.stride) return CRDT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    Table t{nullptr, row_bytes};
+    HIPALLOC(hipMalloc(&t.base, c->cap * (uint64_t)row_bytes));
+    if (c->cap) {
+        k_relayout<<<std::min<uint32_t>(grid_for(c->cap, 256), 65536), 256, 0, c->stream>>>(c->table, t, c->cap);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    hipFree(c->table.base);
+    c->table = t;
     return CRDT_OK;
 }
 
@@ -2296,7 +2328,7 @@ int crdt_refresh_canonical(crdt_ctx* c, uint64_t n_rows, int64_t* out_lt) {
     k_fill_i64<<<1, 64, 0, c->stream>>>(c->d_word.p, 1, INT64_MIN);
     if (n_rows) {
         const unsigned g = std::min<unsigned>(grid_for(n_rows, 256), 2048);
-        k_refresh<<<g, 256, 0, c->stream>>>(c->table.hot, n_rows, c->d_word.p);
+        k_refresh<<<g, 256, 0, c->stream>>>(c->table, n_rows, c->d_word.p);
         HIPCHK(hipGetLastError());
     }
     long long w = 0;
@@ -2333,8 +2365,7 @@ int crdt_clear_rows(crdt_ctx* c, uint64_t first, uint64_t count) {
     if (!c || first > c->cap || count > c->cap - first) return CRDT_E_INVALID;
     if (count == 0) return CRDT_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(c->table.hot + first, 0x80, count * sizeof(Row), c->stream));
-    HIPCHK(hipMemsetAsync(c->table.cold + first, 0x80, count * sizeof(RowX), c->stream));
+    HIPCHK(hipMemsetAsync(row_ptr(c->table, first), 0x80, count * c->table.stride, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
 }
@@ -2346,7 +2377,7 @@ int crdt_remap_ranks(crdt_ctx* c, uint64_t n_rows, const uint32_t* old_to_new, u
     const uint32_t* dl;
     int st;
     if ((st = stage(c, c->s_rank, old_to_new, n_ranks, CRDT_MEM_HOST, &dl))) return st;
-    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table.hot, n_rows, dl, n_ranks);
+    k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table, n_rows, dl, n_ranks);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;

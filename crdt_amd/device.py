@@ -273,6 +273,11 @@ class DeviceTable:
         bucket in any order (same rows / canonical / status; both counts reported as 2^64 - 1)."""
         self._check(self._lib.crdt_set_counts(self._ctx, 1 if exact else 0), "crdt_set_counts")
 
+    def set_row_bytes(self, row_bytes: int):
+        """crdt_set_row_bytes: 24-B rows (default; sorted-path fan-ins) or 32-B rows (gather-path
+        streaming). Same results."""
+        self._check(self._lib.crdt_set_row_bytes(self._ctx, int(row_bytes)), "crdt_set_row_bytes")
+
     def reserve_scratch(self, n_records: int):
         """crdt_reserve_scratch: size the sorted path's partition buffers up front."""
         self._check(self._lib.crdt_reserve_scratch(self._ctx, int(n_records)), "crdt_reserve_scratch")

@@ -128,6 +128,11 @@ int crdt_reserve(crdt_ctx* ctx, uint64_t capacity);          /* grow; new rows a
  * (two partitioned copies, <= 40 B per record), so the first large merge allocates nothing and the
  * buffers are placed while device memory is still unfragmented.  Optional. */
 int crdt_reserve_scratch(crdt_ctx* ctx, uint64_t n_records);
+/* Row size of the device table: 24 (default) or 32 bytes; the rows are copied over.  24-B rows move
+ * 25 % fewer bytes in the sorted path's coalesced passes (many-changeset fan-ins); 32-B rows make
+ * the gather path's random winner writes one aligned 32-B store (streaming calls where most
+ * records win).  Results are identical. */
+int crdt_set_row_bytes(crdt_ctx* ctx, uint32_t row_bytes);
 int crdt_capacity(const crdt_ctx* ctx, uint64_t* out);
 int crdt_set_local_rank(crdt_ctx* ctx, uint32_t rank);        /* after a rank remap */
 

@@ -199,6 +199,38 @@ def test_key_out_of_range_is_reported_not_faulting(gpu_device):
                 np.array([0, 0], np.uint32), np.array([0, 2], np.uint64), 1 << 40)
 
 
+@pytest.mark.parametrize("path", ["gather", "sorted"])
+def test_row_bytes_32_and_relayout(gpu_device, path):
+    """crdt_set_row_bytes: 32-B rows give the oracle's rows on both paths, and switching the row
+    size of a populated table (24 -> 32 -> 24) keeps every row."""
+    from crdt_amd import DeviceTable
+    case = make_case(seed=61, R=80, per_cs=1200, n_local=3000, n_new=1500, millis_span=4, counter_span=2,
+                     n_ranks=7, tomb_frac=0.1)
+    t = DeviceTable(0, local_rank=case["local_rank"], capacity=case["n_ids"])
+    t.set_row_bytes(32)
+    t.set_merge_path(path)
+    if path == "sorted":
+        t.set_counts(False)
+    loc = case["local"]
+    keep = loc["mod"] != ABSENT_MOD
+    ids = np.arange(case["n_local"], dtype=np.uint32)[keep]
+    t.put_rows(ids, loc["lt"][keep], loc["rank"][keep], loc["val"][keep], loc["mod"][keep])
+    t.canonical = case["c0"]
+    t.merge(case["key"], case["lt"], case["rank"], case["val"], case["offsets"], case["wall"],
+            millis=case["millis"], win_flags=False)
+    orows, _, _ = oracle_run(case)
+    all_ids = np.arange(case["n_ids"], dtype=np.uint32)
+    for f, a in zip(("lt", "rank", "val", "mod"), t.read_rows(all_ids)):
+        assert np.array_equal(a, orows[f]), f
+    t.set_row_bytes(24)
+    for f, a in zip(("lt", "rank", "val", "mod"), t.read_rows(all_ids)):
+        assert np.array_equal(a, orows[f]), f
+    t.set_row_bytes(32)
+    for f, a in zip(("lt", "rank", "val", "mod"), t.read_rows(all_ids)):
+        assert np.array_equal(a, orows[f]), f
+    t.close()
+
+
 def test_reserve_preserves_rows(gpu_device):
     from crdt_amd import DeviceTable
     t = DeviceTable(0, local_rank=0, capacity=16)
