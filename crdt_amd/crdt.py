@@ -364,6 +364,63 @@ class MapCrdt(Crdt):
     def merge(self, remoteRecords: dict, wall: int | None = None):    # crdt.dart:77-94
         self.mergeAll([remoteRecords], wall=wall)
 
+    def mergeAllBulk(self, changesets, wall: int | None = None):
+        """The catch-up form of ``mergeAll``: the same R sequential merges (rows, canonical clock,
+        exceptions), but the merged maps are not cut down to their winners (``removeWhere``,
+        crdt.dart:80-85) and no ``watch()`` event is emitted, so no per-record outcome is needed and
+        the device may take the sorted path's order-free form.  Mirrors
+        ``GpuMapCrdt.mergeAllBulk`` (dart/lib/src/gpu_map_crdt.dart).  A batch that needs per-record
+        host bookkeeping — an Hlc outside the (millis << 16) + counter form, or a key whose stored
+        Hlc / modified is kept on the host — runs as ``mergeAll``."""
+        wall = self._wall(wall)
+        changesets = list(changesets)
+        R = len(changesets)
+        if R == 0:
+            return
+        if self._hlc_override or self._mod_override or any(
+                not r.hlc.is_canonical_form for cs in changesets for r in cs.values()):
+            keyed = set(self._hlc_override) | set(self._mod_override)
+            if any(not r.hlc.is_canonical_form for cs in changesets for r in cs.values()) or any(
+                    self._keys.get(k) in keyed for cs in changesets for k in cs):
+                self.mergeAll([dict(cs) for cs in changesets], wall=wall)   # (copies: maps untouched)
+                return
+        self._register_nodes([r.hlc.nodeId for cs in changesets for r in cs.values()])
+        n_total = sum(len(cs) for cs in changesets)
+        kid = np.empty(n_total, np.uint32)
+        lt = np.empty(n_total, np.int64)
+        rank = np.empty(n_total, np.uint32)
+        val = np.empty(n_total, np.uint32)
+        offsets = np.zeros(R + 1, np.uint64)
+        newid_start = []
+        i = 0
+        for j, cs in enumerate(changesets):
+            newid_start.append(len(self._keys))
+            for key, rec in cs.items():
+                kid[i] = self._keys.intern(key)
+                lt[i] = rec.hlc.logicalTime
+                rank[i] = self._nodes.rank(rec.hlc.nodeId)
+                val[i] = self._values.put(rec.value)
+                i += 1
+            offsets[j + 1] = i
+        newid_start.append(len(self._keys))
+        self._reserve()
+        self._table.set_counts(False)
+        try:
+            res, _ = self._table.merge(kid, lt, rank, val, offsets, wall, win_flags=False)
+        except CrdtNativeError:
+            self._keys.truncate(newid_start[0])
+            self._values.release_many(val)
+            raise
+        finally:
+            self._table.set_counts(True)
+        stop = res["n_stored"]
+        self._keys.truncate(newid_start[stop])
+        self._values.release_many(val[int(offsets[stop]):])       # changesets never stored
+        # the stored changesets' losing handles are unknown here: the next compaction frees them
+        self._maybe_compact()
+        self._raise_for(res)
+        return res
+
     def mergeAll(self, changesets, wall: int | None = None):
         """``for m in changesets: merge(m)`` as ONE device call (R sequential merges)."""
         wall = self._wall(wall)

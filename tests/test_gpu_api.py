@@ -533,6 +533,61 @@ def test_batch_with_wide_counter_then_normal_records(gpu_device, drift_at):
     _state_equal(dev, ora)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_merge_all_bulk_sorted_vs_oracle(gpu_device, seed):
+    """MapCrdt.mergeAllBulk on the sorted path (order-free form, forced: the batch is small):
+    recordMap (hlc, value, modified), canonical and the exception equal the oracle's sequential
+    merges and MapCrdt.mergeAll's — ties on (lt, node) across changesets, tombstones, new and
+    seeded keys, a drift in a late changeset for seed 1."""
+    import random
+    from oracle import crdt_oracle as O
+    rnd = random.Random(seed)
+    nodes = ["n%d" % k for k in range(6)]
+    seed_o = {f"k{i}": O.Record(O.Hlc(WALL - 500 + rnd.randrange(8), rnd.randrange(3), rnd.choice(nodes)), i,
+                                O.Hlc(WALL - 400, 0, "local")) for i in range(300)}
+    css_o = []
+    for j in range(70):
+        cs = {}
+        for x, i in enumerate(rnd.sample(range(600), 90)):
+            ms = WALL - 300 + rnd.randrange(6)
+            if seed == 1 and j == 55 and x == 40:
+                ms = WALL + 60_001
+            cs[f"k{i}"] = O.Record(O.Hlc(ms, rnd.randrange(3), rnd.choice(nodes)),
+                                   None if rnd.random() < 0.1 else j * 1000 + i, O.Hlc(0, 0, "local"))
+        css_o.append(cs)
+
+    def to_dev(cs):
+        return {k: Record(Hlc(r.hlc.millis, r.hlc.counter, r.hlc.node_id), r.value,
+                          Hlc(r.modified.millis, r.modified.counter, r.modified.node_id)) for k, r in cs.items()}
+
+    results = []
+    for form in ("bulk", "all", "oracle"):
+        if form == "oracle":
+            m = O.MapCrdt("local", seed_o)
+        else:
+            m = MapCrdt("local", to_dev(seed_o))
+            m._table.set_merge_path("sorted" if form == "bulk" else "gather")
+        exc = None
+        try:
+            if form == "oracle":
+                for cs in css_o:
+                    m.merge(dict(cs), WALL)
+            elif form == "bulk":
+                m.mergeAllBulk([to_dev(cs) for cs in css_o], wall=WALL)
+            else:
+                m.mergeAll([to_dev(cs) for cs in css_o], wall=WALL)
+        except Exception as ex:  # noqa: BLE001
+            exc = type(ex).__name__
+        if form == "bulk":
+            assert m._table.last_path() == "sorted"
+        results.append((m, exc))
+    (bulk, e_b), (allm, e_a), (ora, e_o) = results
+    assert e_b == e_a == e_o
+    assert (e_o is not None) == (seed == 1)
+    _state_equal(bulk, ora)
+    _state_equal(allm, ora)
+
+
 def test_c_abi_from_a_plain_c_host(gpu_device):
     """tests/c/abi_golden.c (built by build()): the library loaded by a C program with no Python
     or torch in it — golden cases through crdt_merge (gather + flags, sorted, and a 1-rank sharded
