@@ -446,8 +446,11 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
       final stop = res.ref.nStored;
       _truncateKeys(newIdStart[stop]); // keys first seen in changesets never stored
       final storedEnd = offsets[stop];
-      if (!winners) {                  // bulk form: no per-record outcome; handles of the batch stay
-        _rethrow(res);                 // referenced until a compaction (values of losers unknown)
+      if (!winners) {                  // bulk form: no per-record outcome; the stored changesets'
+        for (var x = storedEnd; x < n; ++x) {   // handles stay referenced (losers unknown), the
+          _values.release(val[x]);              // unstored ones are released
+        }
+        _rethrow(res);
         return;
       }
       final won = Uint8List.fromList(flags.asTypedList(n == 0 ? 1 : n));
@@ -487,8 +490,26 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   /// A bulk catch-up merge that needs neither the removeWhere side effect nor watch()
   /// events: no win flags, per-record counts off, so crdt_merge may take the sorted path in
   /// its order-free form (same rows, canonical and exceptions; DESIGN.md §5.2).
+  ///
+  /// A batch that needs per-record host bookkeeping — an Hlc outside the (millis << 16) + counter
+  /// form, or a key whose stored Hlc / modified is kept on the host — runs as [mergeAll] on copies
+  /// of the maps (mirrors MapCrdt.mergeAllBulk in crdt_amd/crdt.py).
   void mergeAllBulk(List<Map<K, Record<V>>> changesets) {
+    bool hostKept(K k) {
+      final id = _keyIds[k];
+      return id != null && (_hlcOverride.containsKey(id) || _modOverride.containsKey(id));
+    }
+
+    final needsHost = changesets.any((cs) => cs.entries.any((e) => !_canonicalForm(e.value.hlc) || hostKept(e.key)));
+    if (needsHost) {
+      mergeAll([for (final cs in changesets) Map<K, Record<V>>.of(cs)]);
+      return;
+    }
     _check(_lib.setCounts(_c, 0), 'crdt_set_counts');
-    mergeAll(changesets, winners: false);
+    try {
+      mergeAll(changesets, winners: false);
+    } finally {
+      _check(_lib.setCounts(_c, 1), 'crdt_set_counts');
+    }
   }
 }
