@@ -7,6 +7,8 @@
  *   2. crdt_merge without flags on the sorted path (CRDT_PATH_SORTED, order-free form),
  *   3. crdt_merge on a 1-rank sharded ctx joined to an in-process loopback crdt_comm_ops table
  *      (CRDT_MEM_HOST) — the library's collective path with its exchanges done by this file,
+ *   4. the sorted path again on 32-B rows (crdt_set_row_bytes) with the batch's rank bound declared
+ *      (crdt_set_rank_bound: max rank + 1),
  * and compares status, stop point, exception fields, canonical, win flags and every row with
  * the expected values, bit for bit.  Exit status 0 = all equal.
  *
@@ -142,11 +144,21 @@ static int check(const Case* c, crdt_ctx* ctx, int rc, const crdt_result* res, c
 #undef EXPECT
 }
 
-/* mode 0: gather + flags; 1: sorted, no flags; 2: 1-rank sharded ctx over the loopback table */
+/* mode 0: gather + flags; 1: sorted, no flags; 2: 1-rank sharded ctx over the loopback table;
+ * 3: sorted on 32-B rows with a declared rank bound */
 static int run(const Case* c, int mode) {
     crdt_ctx* ctx = NULL;
     int st = crdt_create(0, c->local_rank, c->n_ids, &ctx);
     if (st != CRDT_OK) { fprintf(stderr, "crdt_create: %s\n", crdt_status_string(st)); return 1; }
+    if (mode == 3) {
+        uint32_t bound = 0;
+        for (uint64_t i = 0; i < c->n; ++i) if (c->rank[i] + 1 > bound) bound = c->rank[i] + 1;
+        if ((st = crdt_set_row_bytes(ctx, 32)) != CRDT_OK || (st = crdt_set_rank_bound(ctx, bound)) != CRDT_OK) {
+            fprintf(stderr, "mode 3 setup: %s\n", crdt_status_string(st));
+            crdt_destroy(ctx);
+            return 1;
+        }
+    }
     uint32_t* ids = malloc(sizeof(uint32_t) * (c->n_local ? c->n_local : 1));
     int64_t *lt = malloc(8 * (c->n_local + 1)), *mod = malloc(8 * (c->n_local + 1));
     uint32_t *rk = malloc(4 * (c->n_local + 1)), *vl = malloc(4 * (c->n_local + 1));
@@ -164,11 +176,11 @@ static int run(const Case* c, int mode) {
     b.key_id = c->key; b.lt = c->lt; b.rank = c->rank; b.val = c->val; b.millis = c->millis;
     b.offsets = c->offsets; b.n_changesets = c->R; b.mem = CRDT_MEM_HOST;
     uint8_t* flags = NULL;
-    const char* what = mode == 0 ? "gather" : mode == 1 ? "sorted" : "sharded-1";
+    const char* what = mode == 0 ? "gather" : mode == 1 ? "sorted" : mode == 2 ? "sharded-1" : "sorted-32B-bound";
     if (mode == 0) {
         crdt_set_merge_path(ctx, CRDT_PATH_GATHER);
         flags = calloc(c->n ? c->n : 1, 1);
-    } else if (mode == 1) {
+    } else if (mode == 1 || mode == 3) {
         crdt_set_merge_path(ctx, CRDT_PATH_SORTED);
         crdt_set_counts(ctx, 0);
     } else {
@@ -187,7 +199,7 @@ static int run(const Case* c, int mode) {
     const int calls0 = lb_calls;
     const int rc = crdt_merge(ctx, &b, c->wall, flags, &res);
     int counted = 1;
-    if (mode == 1) {                                     /* the order-free sorted form does not count */
+    if (mode == 1 || mode == 3) {                        /* the order-free sorted form does not count */
         int path = 0;
         crdt_last_path(ctx, &path);
         counted = path != CRDT_PATH_SORTED;
@@ -223,10 +235,10 @@ int main(int argc, char** argv) {
     for (uint32_t k = 0; k < nc; ++k) {
         Case c;
         read_case(&c);
-        for (int mode = 0; mode < 3; ++mode, ++runs) bad |= run(&c, mode);
+        for (int mode = 0; mode < 4; ++mode, ++runs) bad |= run(&c, mode);
     }
-    printf("abi_golden: %u cases x 3 modes (gather + flags, sorted, 1-rank sharded over a C loopback "
-           "communicator): %s\n", nc, bad ? "MISMATCH" : "all equal");
+    printf("abi_golden: %u cases x 4 modes (gather + flags, sorted, 1-rank sharded over a C loopback "
+           "communicator, sorted on 32-B rows with a rank bound): %s\n", nc, bad ? "MISMATCH" : "all equal");
     (void)runs;
     return bad ? 1 : 0;
 }

@@ -590,8 +590,9 @@ def test_merge_all_bulk_sorted_vs_oracle(gpu_device, seed):
 
 def test_c_abi_from_a_plain_c_host(gpu_device):
     """tests/c/abi_golden.c (built by build()): the library loaded by a C program with no Python
-    or torch in it — golden cases through crdt_merge (gather + flags, sorted, and a 1-rank sharded
-    ctx over a loopback crdt_comm_ops table written in C), every row compared bit for bit."""
+    or torch in it — golden cases through crdt_merge (gather + flags, sorted, a 1-rank sharded
+    ctx over a loopback crdt_comm_ops table written in C, and sorted on 32-B rows with a declared
+    rank bound), every row compared bit for bit."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
