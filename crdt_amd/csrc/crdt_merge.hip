@@ -1108,6 +1108,7 @@ struct Segs {
 constexpr uint32_t kFormNoWholeLines = 64;   // resolve writes changed rows only (partial lines)
 constexpr uint32_t kFormNoKey8 = 128;        // 16-B final records (4-B key column)
 constexpr uint32_t kFormNoKey16 = 256;       // 16-B level-1 records (4-B key column)
+constexpr uint32_t kFormNoReverse = 512;     // partition tiles all fill their ranges forwards
 
 struct crdt_ctx {
     int device = 0;
@@ -1812,26 +1813,27 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const bool ph = c->timing && s0 == 0;       // phase events: the first window
         if (ph) ev_record(c, ev_window(1, false));
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
+        const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
         if (cols.packed_in && k16)
             k_part_scatter1<true, true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (cols.packed_in)
             k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (k16)
             k_part_scatter1<true, false, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (pk)
             k_part_scatter1<true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else
             k_part_scatter1<false><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         if (ph) ev_record(c, ev_window(1, true));
         if (ph) ev_record(c, ev_window(2, false));
         if (two) {
@@ -1860,20 +1862,20 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint32_t xper2 = c->xcd_map ? (nt2 + kXcds - 1) / kXcds : 0;
             if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
+                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
             else if (pk)
                 if (k16)
                     k_part_scatter2<false, true, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2);
+                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
                 else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
                 else
                     k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
             else
                 k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2);
+                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
         }
         if (ph) ev_record(c, ev_window(2, true));
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
