@@ -1109,6 +1109,7 @@ constexpr uint32_t kFormNoWholeLines = 64;   // resolve writes changed rows only
 constexpr uint32_t kFormNoKey8 = 128;        // 16-B final records (4-B key column)
 constexpr uint32_t kFormNoKey16 = 256;       // 16-B level-1 records (4-B key column)
 constexpr uint32_t kFormNoReverse = 512;     // partition tiles all fill their ranges forwards
+constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, shared bins (k_part_hist)
 
 struct crdt_ctx {
     int device = 0;
@@ -1849,7 +1850,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                                             c->p_tseg.p);
             const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            if (k16)   // key bits [4, 20) in 2 B: the level-2 digit (key bits [12, 20)) is its high byte
+            if (k16 && !(c->form_off & kFormNoHistW))   // key bits [4, 20) in 2 B: the level-2 digit
+                k_part_hist16w<<<nt2, kHThreads, 0, c->stream>>>(         // (bits [12, 20)) is its high byte
+                    reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, c->p_hist.p);
+            else if (k16)
                 k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap,
                                                                           kSBits - 4, c->p_hist.p);
             else
