@@ -220,6 +220,7 @@ def main():
             delta_cols.append((src["key"][b:e], src["lt"][b:e], src["rank"][b:e], src["val"][b:e],
                                np.array([0, e - b], np.uint64)))
     table_timing = [False, []]                     # per-call timing records (streaming config)
+    ab_ph = {}                                     # A/B: per-value phase timings of each step
 
     def timed_run(steps):
         step_ms, tsum, res = [], {}, None
@@ -245,6 +246,8 @@ def main():
                 tm["apply_total"] = int(round(tm["apply_total"] * f))
             for k, v in tm.items():
                 tsum[k] = tsum.get(k, 0) + v
+            if ab:
+                ab_ph.setdefault(ab[1][si % len(ab[1])], []).append(tm)
         table.set_timing(False)
         table_timing[0] = False
         return step_ms, tsum, res
@@ -258,6 +261,11 @@ def main():
         for v, ms in ab[2].items():
             log(f"A/B {ab[0]}={v}: mean {np.mean(ms):.3f} ms  min {np.min(ms):.3f}  max {np.max(ms):.3f}  "
                 f"({len(ms)} steps)")
+            ph = ab_ph.get(v, [])
+            if ph:
+                log(f"A/B {ab[0]}={v} phases: " + "  ".join(
+                    f"{k} {np.mean([t[k] for t in ph]):.3f}" for k in ph[0]
+                    if k.endswith("_ms") and isinstance(ph[0][k], (int, float))))
         os.environ.pop(ab[0], None)
     assert res["status"] == 0, res
     ms_per_step = float(np.mean(step_ms))
