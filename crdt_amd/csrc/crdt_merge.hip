@@ -128,6 +128,9 @@ struct Misc {
     //   fr_rlo = max(~rank), fr_rhi = max(rank)
     unsigned long long fr_lo, fr_hi;
     uint32_t fr_rlo, fr_rhi;
+    // one past the largest in-range key id the call read (k_scan<.., kHist>, k_put_*): the
+    // table's high-water mark of written rows moves to it (crdt_ctx::hw)
+    unsigned long long key_end, key_pad;
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
@@ -145,6 +148,24 @@ __device__ inline int64_t wave_max(int64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = imax(v, __shfl_xor(v, off, 64));
     return v;
+}
+
+// *dst = max(*dst, max of v over a 256-thread workgroup): one atomic per workgroup, and only
+// where it moves the value.  Every thread of the workgroup calls it (it has barriers).
+__device__ inline void block_raise_u64(unsigned long long v, unsigned long long* dst) {
+    __shared__ unsigned long long s_v[4];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    if ((threadIdx.x & 63) == 0) s_v[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) v = s_v[w] > v ? s_v[w] : v;
+        if (v > *(volatile unsigned long long*)dst) atomicMax(dst, v);
+    }
+    __syncthreads();
 }
 
 __device__ inline int64_t wave_scan_max_incl(int64_t v, int lane) {
@@ -225,6 +246,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr uint32_t kStep = kHist ? kHistSub : 1u;
+    unsigned long long kend = 0;                   // kHist: one past the largest in-range key read
     for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
       if (kHist) {
         s_h[threadIdx.x] = 0;
@@ -255,6 +277,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             for (int q = 0; q < kScanItems; ++q) {
                 const uint32_t k = kk[kHist ? q : 0];
                 digit_count(s_h, (k >> sh.shift) & 255u, k < sh.cap, lane);
+                if (k < sh.cap && k + 1ull > kend) kend = k + 1ull;
             }
         }
         // rank / millis matter only for records above C0 (the only ones recv() can raise on)
@@ -323,6 +346,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
       }
       if (kHist) sh.hist[(uint64_t)(sh.ptb[j] + u) * 256 + threadIdx.x] = s_h[threadIdx.x];
     }
+    if (kHist) block_raise_u64(kend, &misc->key_end);   // (measured free: in-process A/B)
 }
 
 // M_j = max of changeset j's tile maxima (INT64_MIN when empty).  One block per changeset
@@ -900,11 +924,16 @@ __global__ __launch_bounds__(256) void k_put_rows(
     const uint32_t* __restrict__ val, const int64_t* __restrict__ mod, uint64_t n, Table table,
     uint64_t cap, Misc* __restrict__ misc)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = key[i];
-    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    store_row(table, k, lt[i], rank[i], val[i], mod[i]);
+    unsigned long long kend = 0;                  // grid-stride (capped grid): few key_end atomics
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = key[i];
+        if (k >= cap) { bad = true; continue; }
+        store_row(table, k, lt[i], rank[i], val[i], mod[i]);
+        kend = k + 1ull > kend ? k + 1ull : kend;
+    }
+    if (bad) atomicOr(&misc->err, 1u);
+    block_raise_u64(kend, &misc->key_end);
 }
 
 // put/putAll rows (crdt.dart:41-42, 51-53): hlc = modified = the one send() result.
@@ -912,11 +941,16 @@ __global__ __launch_bounds__(256) void k_put_stamped(
     const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n, int64_t stamp,
     uint32_t local_rank, Table table, uint64_t cap, Misc* __restrict__ misc)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = key[i];
-    if (k >= cap) { atomicOr(&misc->err, 1u); return; }
-    store_row(table, k, stamp, local_rank, val[i], stamp);
+    unsigned long long kend = 0;
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = key[i];
+        if (k >= cap) { bad = true; continue; }
+        store_row(table, k, stamp, local_rank, val[i], stamp);
+        kend = k + 1ull > kend ? k + 1ull : kend;
+    }
+    if (bad) atomicOr(&misc->err, 1u);
+    block_raise_u64(kend, &misc->key_end);
 }
 
 __global__ __launch_bounds__(256) void k_read_rows(
@@ -1110,6 +1144,8 @@ constexpr uint32_t kFormNoKey8 = 128;        // 16-B final records (4-B key colu
 constexpr uint32_t kFormNoKey16 = 256;       // 16-B level-1 records (4-B key column)
 constexpr uint32_t kFormNoReverse = 512;     // partition tiles all fill their ranges forwards
 constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, shared bins (k_part_hist)
+constexpr uint32_t kFormNoHw = 2048;         // packed resolve reads every row (ignores the high-water mark)
+constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
     int device = 0;
@@ -1158,6 +1194,14 @@ struct crdt_ctx {
     uint32_t apply_total = 0;
     // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
     int merge_path = 0;
+    // High-water mark of written rows: every row >= hw holds the never-written fill (0x80 bytes),
+    // so the packed resolve synthesises those rows instead of reading them.  Raised by every row
+    // store (put: the keys' bound; merge: the batch's key bound when the scan read the keys, else
+    // the whole table), lowered by crdt_clear_rows of a range reaching it.
+    uint64_t hw = 0;
+    uint64_t hw_read = 0;           // the mark the current merge's kernels rely on (hw at its start)
+    uint64_t hw_next = 0;           // hw after the current merge (the capacity unless tightened)
+    bool key_end_valid = false;     // this merge's scan reduced the batch's key bound (Misc::key_end)
     DBuf<u32x4> p1_rec, p2_rec;        // 16-B partitioned records {lt, rank, val}
     DBuf<uint32_t> p1_kj, p2_kj;       // and their kj words
     DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
@@ -1191,6 +1235,7 @@ struct crdt_ctx {
     bool last_packed = false;       // the last sorted apply used the packed form
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
+    bool last_hw = false;           // ... whose packed resolve skipped the rows >= hw_read
     bool keys_checked = false;      // the gather apply checked every key id before storing
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
@@ -1342,6 +1387,10 @@ inline size_t events_for(size_t nsegs) {     // (windows 1..3 also bracket the s
     return std::max(ev_window(nsegs / kTimingStride + 2, true), ev_window(3, true)) + 1;
 }
 
+inline void raise_hw(crdt_ctx* c, uint64_t key_end) {
+    c->hw = std::max<uint64_t>(c->hw, std::min<uint64_t>(key_end, c->cap));
+}
+
 inline void ev_record(crdt_ctx* c, size_t idx) {
     if (c->timing && idx < c->events.size()) hipEventRecord(c->events[idx], c->stream);
 }
@@ -1390,6 +1439,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     if (hist) {
         HIPALLOC(c->p_hist1.ensure(c->plan_ptiles * kDigits));
         c->hist1_fused = true;
+        c->key_end_valid = true;
         c->hist1_key = home->key_id;
         c->hist1_shift = c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
     }
@@ -1548,6 +1598,8 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
     HIPCHK(hipStreamSynchronize(c->stream));
     crdt_result res = c->h_misc->result;
     c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
+    if (c->key_end_valid && !c->has_comm)        // stored rows are keys of the batch: below its bound
+        c->hw_next = std::max<uint64_t>(c->hw, std::min<uint64_t>(c->h_misc->key_end, c->cap));
     uint64_t np = 0, nw = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
     bool all_counted = counted, err = c->h_misc->err != 0;
@@ -1732,6 +1784,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
     c->last_key16 = k16;
+    c->last_hw = pk && !c->counts && c->hw_read < c->cap;
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -1916,25 +1969,25 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
             if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             else
                 k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
-                d_hot, d_ib, d_hb, c->table, c->cap, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
+                d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             if (c->form_off & kFormNoWholeLines)
                 k_resolve_packed<false, false><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             else if (k8)
                 k_resolve_packed<false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             else
                 k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->d_Rj.p, jb, ps_key, ps_val,
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
@@ -2241,10 +2294,12 @@ int crdt_put_rows(crdt_ctx* c, const uint32_t* key_id, const int64_t* lt, const 
     if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
     if ((st = stage(c, c->s_mod, mod, n, mem, &dm))) return st;
     if ((st = reset_misc(c))) return st;
-    k_put_rows<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dl, dr, dv, dm, n, c->table, c->cap, c->d_misc);
+    k_put_rows<<<std::min<uint32_t>(grid_for(n, 256), kPutGrid), 256, 0, c->stream>>>(dk, dl, dr, dv, dm, n,
+                                                                                     c->table, c->cap, c->d_misc);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    raise_hw(c, c->h_misc->key_end);
     return c->h_misc->err ? CRDT_E_KEY_RANGE : CRDT_OK;
 }
 
@@ -2280,11 +2335,12 @@ int crdt_put_stamped(crdt_ctx* c, const uint32_t* key_id, const uint32_t* val, u
     if ((st = stage(c, c->s_key, key_id, n, mem, &dk))) return st;
     if ((st = stage(c, c->s_val, val, n, mem, &dv))) return st;
     if ((st = reset_misc(c))) return st;
-    k_put_stamped<<<grid_for(n, 256), 256, 0, c->stream>>>(dk, dv, n, stamp, c->local_rank, c->table, c->cap,
-                                                           c->d_misc);
+    k_put_stamped<<<std::min<uint32_t>(grid_for(n, 256), kPutGrid), 256, 0, c->stream>>>(
+        dk, dv, n, stamp, c->local_rank, c->table, c->cap, c->d_misc);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    raise_hw(c, c->h_misc->key_end);
     if (c->h_misc->err) return CRDT_E_KEY_RANGE;
     c->canonical = stamp;
     res.canonical_lt = stamp;
@@ -2373,6 +2429,7 @@ int crdt_clear_rows(crdt_ctx* c, uint64_t first, uint64_t count) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(row_ptr(c->table, first), 0x80, count * c->table.stride, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (first <= c->hw && first + count >= c->hw) c->hw = first;   // the rows from first on are fill
     return CRDT_OK;
 }
 
@@ -2384,6 +2441,7 @@ int crdt_remap_ranks(crdt_ctx* c, uint64_t n_rows, const uint32_t* old_to_new, u
     int st;
     if ((st = stage(c, c->s_rank, old_to_new, n_ranks, CRDT_MEM_HOST, &dl))) return st;
     k_remap<<<grid_for(n_rows, 256), 256, 0, c->stream>>>(c->table, n_rows, dl, n_ranks);
+    if (n_ranks > 0x80808080u) raise_hw(c, n_rows);      // the fill's rank 0x80808080 would be remapped
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return CRDT_OK;
@@ -2404,6 +2462,15 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     }
     HIPCHK(hipSetDevice(c->device));
     if (c->env_dynamic) read_env_knobs(c);
+    // rows >= hw_read are read as the fill by this merge; afterwards hw moves to hw_next (the
+    // capacity unless finish_apply learned the batch's key bound) on every return path
+    c->hw_read = (c->form_off & kFormNoHw) ? c->cap : c->hw;
+    c->hw_next = c->cap;
+    c->key_end_valid = false;
+    struct HwUpdate {
+        crdt_ctx* c;
+        ~HwUpdate() { c->hw = std::max(c->hw, c->hw_next); }
+    } hw_update{c};
     if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
     // Host batches are staged once; every phase then sees device columns.
     crdt_batch dev = *batch;
@@ -2491,6 +2558,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_hist1_fused) f |= CRDT_PLAN_HIST_IN_SCAN;
         if (c->last_key8) f |= CRDT_PLAN_KEY8;
         if (c->last_key16) f |= CRDT_PLAN_KEY16;
+        if (c->last_hw) f |= CRDT_PLAN_HIGH_WATER;
     }
     *flags = f;
     return CRDT_OK;

@@ -296,7 +296,8 @@ class DeviceTable:
         self._check(self._lib.crdt_last_path(self._ctx, ctypes.byref(v)), "crdt_last_path")
         return {1: "gather", 2: "sorted"}[v.value]
 
-    PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32}
+    PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32,
+                  "high_water": 64}
 
     def last_plan(self) -> dict:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""

@@ -271,7 +271,9 @@ enum crdt_plan_flags {
     CRDT_PLAN_TWO_LEVEL = 4,     /* ... with two partition levels (capacity > 2^20) */
     CRDT_PLAN_HIST_IN_SCAN = 8,  /* ... with its level-1 histogram counted by the scan */
     CRDT_PLAN_KEY8 = 16,         /* ... with 13-B final records (1-B key column, 4 key bits in the packed key) */
-    CRDT_PLAN_KEY16 = 32         /* ... and 14-B level-1 records (2-B key column) */
+    CRDT_PLAN_KEY16 = 32,        /* ... and 14-B level-1 records (2-B key column) */
+    CRDT_PLAN_HIGH_WATER = 64    /* ... and its resolve did not read the rows at or above the table's
+                                    high-water mark of written rows (never-written fill) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

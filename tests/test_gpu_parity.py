@@ -897,3 +897,98 @@ def test_more_changesets_than_grid_rows(gpu_device):
     """R = 70,000 changesets (> 65,535: the scan's grid.y loops; > the fused clock's limit)."""
     compare_with_oracle(make_case(seed=4300, R=70_000, per_cs=2, n_local=300, n_new=200, millis_span=4000,
                                   counter_span=2, n_ranks=9))
+
+
+@pytest.mark.parametrize("form_off", ["0", "2048"])
+def test_high_water_mark_sequence(gpu_device, monkeypatch, form_off):
+    """The table's high-water mark of written rows (crdt_ctx::hw: rows at or above it are the
+    never-written fill, so the packed resolve synthesises them instead of reading them) across a
+    sequence of stores: put_rows (host and device keys), sorted merges whose rows lie above the
+    previous mark, clear_rows reaching the mark, a gather-path merge (mark -> capacity), put_stamped
+    — every row and the canonical equal to the C oracle after each step; bit 2048 of
+    CRDT_SORTED_FORM reads every row (the same results)."""
+    import torch
+
+    from crdt_amd import DeviceTable
+    from oracle.oracle_c import OracleTable, new_table
+    from tests._cases import WALL
+    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
+    cap, NR = (1 << 21) + 37, 9
+    rng = np.random.default_rng(4242)
+    c0 = (WALL - 5000) << 16
+    t = DeviceTable(0, local_rank=0, capacity=cap)
+    o = OracleTable(cap, 0, c0)
+    t.canonical = c0
+    t.set_rank_bound(NR)
+    t.set_counts(False)
+
+    def rows_equal(tag):
+        lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a, o.rows[f]), (tag, f, np.flatnonzero(a != o.rows[f])[:5])
+        assert t.canonical == o.canonical, tag
+
+    def put(keys, dev):
+        n = len(keys)
+        lt = ((WALL - 3000 + rng.integers(0, 64, n)) << 16) | rng.integers(0, 4, n)
+        rk = rng.integers(0, NR, n).astype(np.uint32)
+        val = rng.integers(0, 1 << 30, n).astype(np.uint32)
+        mod = np.full(n, c0, np.int64)
+        o.put_rows(keys, lt, rk, val, mod)
+        cols = [keys.astype(np.uint32), lt.astype(np.int64), rk, val, mod]
+        if dev:
+            cols = [torch.from_numpy(c.view(np.int32) if c.dtype == np.uint32 else c).cuda() for c in cols]
+        t.put_rows(*cols)
+
+    def batch(R, per, hi):
+        keys = [rng.choice(hi, per, replace=False).astype(np.uint32) for _ in range(R)]
+        key = np.concatenate(keys)
+        n = len(key)
+        lt = ((WALL - 2000 + rng.integers(0, 64, n)) << 16) | rng.integers(0, 4, n)
+        rk = rng.integers(1, NR, n).astype(np.uint32)
+        val = rng.integers(0, 1 << 30, n).astype(np.uint32)
+        offs = np.arange(R + 1, dtype=np.uint64) * per
+        return key, lt.astype(np.int64), rk, val, offs
+
+    def merge(b, path, dev=True, wall=WALL):
+        key, lt, rk, val, offs = b
+        t.set_merge_path(path)
+        o.merge(key, lt, rk, val, offs, wall)
+        cols = [key, lt, rk, val]
+        if dev:
+            cols = [torch.from_numpy(c.view(np.int32) if c.dtype == np.uint32 else c).cuda() for c in cols]
+        res, _ = t.merge(*cols, offs, wall, win_flags=path == "gather")
+        assert res["status"] == 0 and t.last_path() == path
+        return t.last_plan()
+
+    put(np.arange(3000, dtype=np.uint32), dev=True)                      # mark 3000
+    plan = merge(batch(70, 3000, 1_200_000), "sorted")                   # rows up to ~1.2M written
+    assert plan["packed"] and plan["high_water"] == (form_off == "0"), plan
+    rows_equal("A")
+    merge(batch(70, 3000, cap), "sorted")                                 # reads A's rows above 3000
+    rows_equal("B")
+    t.clear_rows(5000, cap - 5000)                                        # mark back to 5000
+    o.rows[5000:] = new_table(cap - 5000)
+    plan = merge(batch(66, 2500, cap), "sorted")
+    assert plan["high_water"] == (form_off == "0"), plan
+    rows_equal("C")
+    merge(batch(3, 2000, cap), "gather", dev=False)                       # mark -> capacity
+    plan = merge(batch(64, 2000, cap), "sorted")
+    assert not plan["high_water"], plan
+    rows_equal("D")
+    t.clear_rows(0, cap)                                                  # mark 0
+    o.rows[:] = new_table(cap)
+    put(np.array([7, cap - 40, 1_500_000], np.uint32), dev=False)         # mark cap - 39
+    merge(batch(64, 2000, cap), "sorted")
+    rows_equal("E")
+    t.clear_rows(0, cap)
+    o.rows[:] = new_table(cap)
+    key = np.array([11, 900_000], np.uint32)
+    val = np.array([5, 6], np.uint32)
+    r1 = t.put_stamped(key, val, WALL)                                    # mark 900,001
+    o.put_stamped(key, val, WALL)
+    assert r1["canonical_lt"] == o.canonical
+    plan = merge(batch(64, 2000, cap), "sorted")
+    assert plan["high_water"] == (form_off == "0"), plan
+    rows_equal("F")
+    t.close()
