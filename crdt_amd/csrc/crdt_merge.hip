@@ -1784,7 +1784,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
     c->last_key16 = k16;
-    c->last_hw = pk && !c->counts && c->hw_read < c->cap;
+    c->last_hw = pk && !c->counts && c->hw_read < c->cap;     // (in the first window)
     for (size_t sb = 0; sb < ns_all;) {
         const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
         size_t se = sb;
@@ -2004,6 +2004,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             c->sorted_phases = true;
         }
         HIPCHK(hipGetLastError());
+        // the next window reads rows this one may have written anywhere below the capacity
+        c->hw_read = c->cap;
     }
     if (c->timing) {
         ev_record(c, ev_window(0, true));
