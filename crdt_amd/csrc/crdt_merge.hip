@@ -128,7 +128,8 @@ struct Misc {
     //   fr_rlo = max(~rank), fr_rhi = max(rank)
     unsigned long long fr_lo, fr_hi;
     uint32_t fr_rlo, fr_rhi;
-    // one past the largest in-range key id the call read (k_scan<.., kHist>, k_put_*): the
+    // a bound of the rows the call wrote (k_put_*: one past the largest in-range key id;
+    // k_bucket_items: the end of the last non-empty 4096-key bucket of the sorted path): the
     // table's high-water mark of written rows moves to it (crdt_ctx::hw)
     unsigned long long key_end, key_pad;
     unsigned long long present[kCounterSlots];
@@ -246,7 +247,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr uint32_t kStep = kHist ? kHistSub : 1u;
-    unsigned long long kend = 0;                   // kHist: one past the largest in-range key read
     for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
       if (kHist) {
         s_h[threadIdx.x] = 0;
@@ -277,7 +277,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             for (int q = 0; q < kScanItems; ++q) {
                 const uint32_t k = kk[kHist ? q : 0];
                 digit_count(s_h, (k >> sh.shift) & 255u, k < sh.cap, lane);
-                if (k < sh.cap && k + 1ull > kend) kend = k + 1ull;
             }
         }
         // rank / millis matter only for records above C0 (the only ones recv() can raise on)
@@ -346,7 +345,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
       }
       if (kHist) sh.hist[(uint64_t)(sh.ptb[j] + u) * 256 + threadIdx.x] = s_h[threadIdx.x];
     }
-    if (kHist) block_raise_u64(kend, &misc->key_end);   // (measured free: in-process A/B)
 }
 
 // M_j = max of changeset j's tile maxima (INT64_MIN when empty).  One block per changeset
@@ -1201,7 +1199,7 @@ struct crdt_ctx {
     uint64_t hw = 0;
     uint64_t hw_read = 0;           // the mark the current merge's kernels rely on (hw at its start)
     uint64_t hw_next = 0;           // hw after the current merge (the capacity unless tightened)
-    bool key_end_valid = false;     // this merge's scan reduced the batch's key bound (Misc::key_end)
+    bool key_end_valid = false;     // this merge's sorted path reduced its bucket bound (Misc::key_end)
     DBuf<u32x4> p1_rec, p2_rec;        // 16-B partitioned records {lt, rank, val}
     DBuf<uint32_t> p1_kj, p2_kj;       // and their kj words
     DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
@@ -1439,7 +1437,6 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     if (hist) {
         HIPALLOC(c->p_hist1.ensure(c->plan_ptiles * kDigits));
         c->hist1_fused = true;
-        c->key_end_valid = true;
         c->hist1_key = home->key_id;
         c->hist1_shift = c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
     }
@@ -1598,7 +1595,7 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
     HIPCHK(hipStreamSynchronize(c->stream));
     crdt_result res = c->h_misc->result;
     c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
-    if (c->key_end_valid && !c->has_comm)        // stored rows are keys of the batch: below its bound
+    if (c->key_end_valid && !c->has_comm)        // rows stored lie in the sorted path's buckets
         c->hw_next = std::max<uint64_t>(c->hw, std::min<uint64_t>(c->h_misc->key_end, c->cap));
     uint64_t np = 0, nw = 0;
     for (int s = 0; s < kCounterSlots; ++s) { np += c->h_misc->present[s]; nw += c->h_misc->won[s]; }
@@ -1777,6 +1774,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
     c->last_packed = pk;
+    c->key_end_valid = true;                 // k_bucket_items bounds the rows every window writes
     c->last_hist1_fused = false;
     c->sorted_phases = false;
     // final records with a 1-B key column when the packed key leaves 4 bits free (two levels)
@@ -1953,7 +1951,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
         if (ph) ev_record(c, ev_window(3, false));
-        k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot);
+        k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
         if (c->counts) {
