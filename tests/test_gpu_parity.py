@@ -992,3 +992,72 @@ def test_high_water_mark_sequence(gpu_device, monkeypatch, form_off):
     assert plan["high_water"] == (form_off == "0"), plan
     rows_equal("F")
     t.close()
+
+
+def test_high_water_mark_reserve_relayout_remap(gpu_device):
+    """The high-water mark across crdt_reserve (new rows are fill above the mark), a relayout to
+    32-B rows (the packed resolve then synthesises 32-B-stride fill rows) and crdt_remap_ranks:
+    sorted merges after each equal the C oracle."""
+    import torch
+
+    from crdt_amd import DeviceTable
+    from oracle.oracle_c import OracleTable, new_table
+    from tests._cases import WALL
+    NR = 7
+    rng = np.random.default_rng(777)
+    c0 = (WALL - 5000) << 16
+    cap0, cap1 = (1 << 20) + 100, (1 << 21) + 3
+    t = DeviceTable(0, local_rank=0, capacity=cap0)
+    t.canonical = c0
+    t.set_rank_bound(NR)
+    t.set_counts(False)
+    t.set_merge_path("sorted")
+    o = OracleTable(cap1, 0, c0)
+
+    def merge(hi, R=64, per=1500):
+        keys = [rng.choice(hi, per, replace=False).astype(np.uint32) for _ in range(R)]
+        key = np.concatenate(keys)
+        n = len(key)
+        lt = (((WALL - 2000 + rng.integers(0, 64, n)) << 16) | rng.integers(0, 4, n)).astype(np.int64)
+        rk = rng.integers(1, NR, n).astype(np.uint32)
+        val = rng.integers(0, 1 << 30, n).astype(np.uint32)
+        offs = np.arange(R + 1, dtype=np.uint64) * per
+        o.merge(key, lt, rk, val, offs, WALL)
+        dev = [torch.from_numpy(c.view(np.int32) if c.dtype == np.uint32 else c).cuda() for c in (key, lt, rk, val)]
+        res, _ = t.merge(*dev, offs, WALL, win_flags=False)
+        assert res["status"] == 0 and t.last_path() == "sorted"
+        return t.last_plan()
+
+    def check(tag):
+        n = min(t.capacity, cap1)                     # (reserve may grow past cap1: fill rows)
+        lt, rk, val, mod = t.read_rows(np.arange(n, dtype=np.uint32))
+        for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
+            assert np.array_equal(a, o.rows[f][:n]), (tag, f)
+        assert t.canonical == o.canonical, tag
+
+    keys = np.arange(2000, dtype=np.uint32)
+    lt = (((WALL - 3000 + rng.integers(0, 64, 2000)) << 16)).astype(np.int64)
+    rk = rng.integers(0, NR, 2000).astype(np.uint32)
+    val = rng.integers(0, 1 << 30, 2000).astype(np.uint32)
+    mod = np.full(2000, c0, np.int64)
+    t.put_rows(keys, lt, rk, val, mod)
+    o.put_rows(keys, lt, rk, val, mod)
+    assert merge(cap0)["high_water"]
+    check("cap0")
+    t.reserve(cap1)                                   # grown: rows [cap0, cap1) are fill
+    assert t.capacity >= cap1
+    assert merge(cap1)["two_level"]
+    check("reserve")
+    t.set_row_bytes(32)
+    t.clear_rows(900_000, t.capacity - 900_000)
+    o.rows[900_000:] = new_table(cap1 - 900_000)
+    assert merge(cap1)["high_water"]
+    check("32-B rows")
+    lut = np.array([0, 2, 1, 4, 3, 6, 5], np.uint32)     # ranks permuted (a node id order change)
+    t.remap_ranks(t.capacity, lut)
+    r = o.rows["rank"]
+    sel = r < len(lut)
+    r[sel] = lut[r[sel]]
+    merge(cap1)
+    check("remap")
+    t.close()
