@@ -1143,6 +1143,7 @@ constexpr uint32_t kFormNoKey16 = 256;       // 16-B level-1 records (4-B key co
 constexpr uint32_t kFormNoReverse = 512;     // partition tiles all fill their ranges forwards
 constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, shared bins (k_part_hist)
 constexpr uint32_t kFormNoHw = 2048;         // packed resolve reads every row (ignores the high-water mark)
+constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load per record and column
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1872,6 +1873,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (cols.packed_in)
             k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+        else if (k16 && !(c->form_off & kFormNoVecLoads))
+            k_part_scatter1<true, false, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (k16)
