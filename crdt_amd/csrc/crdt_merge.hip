@@ -228,7 +228,9 @@ struct ScanHist {
     uint32_t* hist;
 };
 
-template <bool kEager, bool kMillis = true, bool kFrame = false, bool kHist = false>
+// kVec: a thread's records are 4 groups of 4 consecutive ones (lt read with two 16-B loads per
+// group, keys with one) instead of 16 strided ones; every per-tile result is order-free.
+template <bool kEager, bool kMillis = true, bool kFrame = false, bool kHist = false, bool kVec = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
@@ -261,11 +263,34 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         uint32_t rk[kEager ? kScanItems : 1];
         int64_t mv[kEager && kMillis ? kScanItems : 1];
         uint32_t kk[kHist ? kScanItems : 1];
+        auto idx = [&](int q) -> uint64_t {
+            return kVec ? base + (uint64_t)(q >> 2) * (4 * kScanThreads) + threadIdx.x * 4u + (q & 3)
+                        : base + (uint64_t)q * kScanThreads + threadIdx.x;
+        };
+        bool vec_done[kVec ? kScanItems / 4 : 1];
+#pragma unroll
+        for (int g = 0; g < (kVec ? kScanItems / 4 : 0); ++g) {
+            const uint64_t i0 = idx(4 * g);
+            vec_done[kVec ? g : 0] = i0 + 4 <= end;
+            if (i0 + 4 <= end) {
+                const u32x4u a = *reinterpret_cast<const u32x4u*>(lt + i0);
+                const u32x4u b = *reinterpret_cast<const u32x4u*>(lt + i0 + 2);
+                v[4 * g] = (int64_t)(((uint64_t)a.y << 32) | a.x); v[4 * g + 1] = (int64_t)(((uint64_t)a.w << 32) | a.z);
+                v[4 * g + 2] = (int64_t)(((uint64_t)b.y << 32) | b.x); v[4 * g + 3] = (int64_t)(((uint64_t)b.w << 32) | b.z);
+                if (kHist) {
+                    const u32x4u kv = *reinterpret_cast<const u32x4u*>(sh.key + i0);
+                    kk[kHist ? 4 * g : 0] = kv.x; kk[kHist ? 4 * g + 1 : 0] = kv.y;
+                    kk[kHist ? 4 * g + 2 : 0] = kv.z; kk[kHist ? 4 * g + 3 : 0] = kv.w;
+                }
+            }
+        }
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
-            const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
-            v[q] = i < end ? lt[i] : INT64_MIN;
-            if (kHist) kk[kHist ? q : 0] = i < end ? __builtin_nontemporal_load(sh.key + i) : UINT32_MAX;
+            const uint64_t i = idx(q);
+            if (!kVec || !vec_done[kVec ? q >> 2 : 0]) {
+                v[q] = i < end ? lt[i] : INT64_MIN;
+                if (kHist) kk[kHist ? q : 0] = i < end ? __builtin_nontemporal_load(sh.key + i) : UINT32_MAX;
+            }
             if (kEager) {
                 rk[q] = i < end ? rank[i] : 0u;
                 if (kMillis) mv[kMillis ? q : 0] = (millis && i < end) ? millis[i] : 0;
@@ -283,7 +308,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             if (v[q] > c0) {
-                const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+                const uint64_t i = idx(q);
                 const int64_t ms = (kMillis && millis) ? (kEager ? mv[kEager && kMillis ? q : 0] : millis[i])
                                                        : (v[q] >> kShift);
                 const uint32_t r = kEager ? rk[kEager ? q : 0] : rank[i];
@@ -294,7 +319,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         if (kFrame) {
 #pragma unroll
             for (int q = 0; q < kScanItems; ++q) {
-                const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
+                const uint64_t i = idx(q);
                 if (i < end) {
                     const uint64_t o = ord64(v[q]);
                     flo = ~o > flo ? ~o : flo;
@@ -1144,6 +1169,7 @@ constexpr uint32_t kFormNoReverse = 512;     // partition tiles all fill their r
 constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, shared bins (k_part_hist)
 constexpr uint32_t kFormNoHw = 2048;         // packed resolve reads every row (ignores the high-water mark)
 constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load per record and column
+constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1448,7 +1474,12 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gxh = std::max<uint32_t>(1, std::min<uint32_t>((mt + kHistSub - 1) / kHistSub, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (hist)
+            if (hist && !(c->form_off & kFormNoVecScan))
+                k_scan<false, true, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
+                    ScanHist{home->key_id, c->d_ptb, c->cap, c->hist1_shift, c->p_hist1.p});
+            else if (hist)
                 k_scan<false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
