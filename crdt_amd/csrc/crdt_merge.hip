@@ -1899,11 +1899,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
         if (cols.packed_in && k16)
-            k_part_scatter1<true, true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+            k_part_scatter1<true, true, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (cols.packed_in)
-            k_part_scatter1<true, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+            k_part_scatter1<true, true, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (k16 && !(c->form_off & kFormNoVecLoads))
@@ -1915,11 +1915,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (pk)
-            k_part_scatter1<true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+            k_part_scatter1<true, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else
-            k_part_scatter1<false><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+            k_part_scatter1<false, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr);
         if (ph) ev_record(c, ev_window(1, true));
