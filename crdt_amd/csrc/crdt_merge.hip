@@ -1170,6 +1170,7 @@ constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, sh
 constexpr uint32_t kFormNoHw = 2048;         // packed resolve reads every row (ignores the high-water mark)
 constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load per record and column
 constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
+constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1854,7 +1855,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         c->h_pplan.p[tail + 2] = 0;                                   // seg_pos {0}
         HIPCHK(hipMemcpyAsync(c->p_plan.p, c->h_pplan.p, words * sizeof(uint64_t), hipMemcpyHostToDevice,
                               c->stream));
-        const uint32_t nt2 = two ? (uint32_t)((nw + kPTile - 1) / kPTile) + kDigits : 0;
+        const uint32_t nt2 = two ? (uint32_t)((nw + kPTile2 - 1) / kPTile2) + kDigits : 0;
         const uint32_t nc2 = two ? (nt2 + kChunkTiles - 1) / kChunkTiles + kDigits : 0;
         const uint32_t ntm = std::max(nt1, nt2), ncm = std::max(nc1, nc2);
         HIPALLOC(c->p_hist.ensure((size_t)ntm * kDigits));
@@ -1875,7 +1876,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const uint32_t* d_tb1 = d_sj + nseg;
         HIPALLOC(c->p_tseg.ensure(ntm));
         k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1, c->p_tseg.p);
-        const TileMap tm1{d_beg, d_end, d_tb1, c->p_tseg.p, d_sj, nseg};
+        const TileMap tm1{d_beg, d_end, d_tb1, c->p_tseg.p, d_sj, nseg, (uint32_t)kPTile};
         const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tail),
                           reinterpret_cast<const uint32_t*>(c->p_plan.p + tail + 1), c->p_plan.p + tail + 2, 1};
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
@@ -1932,10 +1933,14 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             p2k = c->p2_kj.p + (size_t)c->l2_shift_kb * 256;
             uint32_t* tb2 = c->p_l2map.p;
             uint32_t* cb2 = c->p_l2map.p + kDigits + 1;
-            k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2);
+            // level-2 tiles of the packed form: kPTile2 records (one sub-tile each) — 256 workgroups
+            // then cover a short stretch of each level-1 bucket at a time
+            const uint32_t ts2 = k16 && !(c->form_off & kFormNoHistW) && !(c->form_off & kFormBigTile2)
+                                 ? (uint32_t)kPTile2 : (uint32_t)kPTile;
+            k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2, ts2);
             k_seg_index<<<std::min<uint32_t>(grid_for(nt2, 256), 4096), 256, 0, c->stream>>>(tb2, kDigits, nt2,
                                                                                             c->p_tseg.p);
-            const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits};
+            const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits, ts2};
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
             if (k16 && !(c->form_off & kFormNoHistW))   // key bits [4, 20) in 2 B: the level-2 digit
                 k_part_hist16w<<<nt2, kHThreads, 0, c->stream>>>(         // (bits [12, 20)) is its high byte
@@ -1950,22 +1955,25 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
             k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
             // (nt2 is an upper bound of the level-2 tiles; the real count is on the device)
-            const uint32_t xper2 = c->xcd_map ? (nt2 + kXcds - 1) / kXcds : 0;
+            // (the grid and the XCD-contiguous mapping from a tile bound for THIS tile size: a loose
+            // bound would leave the upper XCDs' ranges past the last tile, idle)
+            const uint32_t nt2s = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
+            const uint32_t xper2 = c->xcd_map ? (nt2s + kXcds - 1) / kXcds : 0;
             if (c->counts)
-                k_part_scatter2<true, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
             else if (pk)
                 if (k16)
-                    k_part_scatter2<false, true, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
                 else if (k8)
-                    k_part_scatter2<false, true, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    k_part_scatter2<false, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
                 else
-                    k_part_scatter2<false, true><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                    k_part_scatter2<false, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
             else
-                k_part_scatter2<false, false><<<xcd_grid(nt2, c->xcd_map), kPThreads, 0, c->stream>>>(
+                k_part_scatter2<false, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
         }
         if (ph) ev_record(c, ev_window(2, true));

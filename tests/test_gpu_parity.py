@@ -693,18 +693,18 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
     t.close()
 
 
-@pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768"])
+@pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536"])
 def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
     level-2 histogram with 2-B loads into shared bins, the level-1 scatter's / the scan's narrow
-    loads) gives the same rows."""
+    loads, 32K-record level-2 tiles) gives the same rows."""
     monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
     case = _frame_edge_case(99)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
-    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768")), res["plan"]
+    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
 
 
 @pytest.mark.parametrize("L", [42, 43, 44, 45])
