@@ -840,6 +840,154 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
     }
 }
 
+// Wave-aggregated slot in a small LDS counter array: the lanes of a wave holding the same
+// destination d (< 2^nbits) find each other by ballots over d's bits; the lowest one adds the group's
+// size with one LDS atomic, every lane gets base + its rank in the group (k_route_*<.., kAgg>: with
+// G <= 8 owners a wave's 64 lanes otherwise hit at most 8 addresses with 64 atomics).
+__device__ inline uint32_t agg_slot(uint32_t* cnt, uint32_t d, bool act, uint32_t nbits, bool want_pos) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long m = __ballot(act);
+    for (uint32_t b = 0; b < nbits; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const unsigned long long bb = __ballot(act && bit);
+        m &= bit ? bb : ~bb;
+    }
+    if (!act) return 0u;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[d], (uint32_t)__popcll(m));
+    if (!want_pos) return 0u;
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+}
+
+// Vector-load variants of the two routing kernels: a thread's 16 records of a scan tile are 4 groups
+// of 4 consecutive ones (16-B key loads; in the scatter also 16-B val / rank and 2 x 16-B lt loads),
+// counted with agg_slot.  Same counts; the scatter's output order inside an (owner, changeset)
+// run differs, which nothing depends on (keys are distinct inside a changeset; win flags travel
+// back through o_perm).
+inline uint32_t route_bits(uint32_t G) {              // bits of the largest owner index
+    uint32_t b = 0;
+    while ((1u << b) < G) ++b;
+    return b;
+}
+
+__device__ inline uint64_t route_idx(uint64_t base, int q) {
+    return base + (uint64_t)(q >> 2) * (4 * kScanThreads) + threadIdx.x * 4u + (q & 3);
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_route_count_v(
+    const uint32_t* __restrict__ key, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
+    uint32_t jbase, uint32_t R, uint32_t G, uint32_t nbits, unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t s_cnt[kRouteMaxRanks];
+    const uint32_t j = jbase + blockIdx.y;
+    const uint64_t beg = offs[j], end = offs[j + 1];
+    const uint32_t nt = tstart[j + 1] - tstart[j];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
+        __syncthreads();
+        const uint64_t base = beg + (uint64_t)t * kTile;
+        uint32_t k[kScanItems];
+#pragma unroll
+        for (int g = 0; g < kScanItems / 4; ++g) {
+            const uint64_t i0 = route_idx(base, 4 * g);
+            if (i0 + 4 <= end) {
+                const u32x4u v = *reinterpret_cast<const u32x4u*>(key + i0);
+                k[4 * g] = v.x; k[4 * g + 1] = v.y; k[4 * g + 2] = v.z; k[4 * g + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int x = 0; x < 4; ++x) k[4 * g + x] = i0 + x < end ? key[i0 + x] : 0u;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q)
+            agg_slot(s_cnt, k[q] % G, route_idx(base, q) < end, nbits, false);
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
+            if (s_cnt[d]) atomicAdd(&counts[(uint64_t)d * R + j], (unsigned long long)s_cnt[d]);
+        __syncthreads();
+    }
+}
+
+template <bool kPk>
+__global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
+    const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
+    uint32_t jbase, uint32_t R, uint32_t G, uint32_t nbits, unsigned long long* __restrict__ cursor,
+    uint32_t* __restrict__ o_slot, int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank,
+    uint32_t* __restrict__ o_val, uint64_t* __restrict__ o_perm, PackFrame pf)
+{
+    __shared__ uint32_t s_cnt[kRouteMaxRanks];
+    __shared__ unsigned long long s_base[kRouteMaxRanks];
+    const uint32_t j = jbase + blockIdx.y;
+    const uint64_t beg = offs[j], end = offs[j + 1];
+    const uint32_t nt = tstart[j + 1] - tstart[j];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads) s_cnt[d] = 0;
+        __syncthreads();
+        const uint64_t base = beg + (uint64_t)t * kTile;
+        uint32_t k[kScanItems], pos[kScanItems];
+#pragma unroll
+        for (int g = 0; g < kScanItems / 4; ++g) {
+            const uint64_t i0 = route_idx(base, 4 * g);
+            if (i0 + 4 <= end) {
+                const u32x4u v = *reinterpret_cast<const u32x4u*>(key + i0);
+                k[4 * g] = v.x; k[4 * g + 1] = v.y; k[4 * g + 2] = v.z; k[4 * g + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int x = 0; x < 4; ++x) k[4 * g + x] = i0 + x < end ? key[i0 + x] : 0u;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q)
+            pos[q] = agg_slot(s_cnt, k[q] % G, route_idx(base, q) < end, nbits, true);
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < G; d += kScanThreads)
+            s_base[d] = s_cnt[d] ? atomicAdd(&cursor[(uint64_t)d * R + j], (unsigned long long)s_cnt[d]) : 0;
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < kScanItems / 4; ++g) {
+            const uint64_t i0 = route_idx(base, 4 * g);
+            int64_t l[4];
+            uint32_t r[4], v[4];
+            if (i0 + 4 <= end) {
+                const u32x4u a = *reinterpret_cast<const u32x4u*>(lt + i0);
+                const u32x4u b = *reinterpret_cast<const u32x4u*>(lt + i0 + 2);
+                l[0] = (int64_t)(((uint64_t)a.y << 32) | a.x); l[1] = (int64_t)(((uint64_t)a.w << 32) | a.z);
+                l[2] = (int64_t)(((uint64_t)b.y << 32) | b.x); l[3] = (int64_t)(((uint64_t)b.w << 32) | b.z);
+                const u32x4u rv = *reinterpret_cast<const u32x4u*>(rank + i0);
+                const u32x4u vv = *reinterpret_cast<const u32x4u*>(val + i0);
+                r[0] = rv.x; r[1] = rv.y; r[2] = rv.z; r[3] = rv.w;
+                v[0] = vv.x; v[1] = vv.y; v[2] = vv.z; v[3] = vv.w;
+            } else {
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    const uint64_t i = i0 + x < end ? i0 + x : beg;
+                    l[x] = lt[i]; r[x] = rank[i]; v[x] = val[i];
+                }
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const int q = 4 * g + x;
+                const uint64_t i = i0 + x;
+                if (i >= end) continue;
+                const uint64_t o = s_base[k[q] % G] + pos[q];
+                o_slot[o] = k[q] / G;
+                if (kPk) {
+                    o_lt[o] = (int64_t)pack_record(pf, l[x], r[x], j % kWindow);
+                } else {
+                    o_lt[o] = l[x];
+                    o_rank[o] = r[x];
+                }
+                o_val[o] = v[x];
+                if (o_perm) o_perm[o] = i;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // Packed routed records back to (lt, rank) columns, for an apply that takes the gather path.
 __global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt, uint32_t* __restrict__ rank,
                                                        uint64_t n, PackFrame pf)
@@ -1170,6 +1318,7 @@ constexpr uint32_t kFormNoHistW = 1024;      // level-2 histogram: 2-B loads, sh
 constexpr uint32_t kFormNoHw = 2048;         // packed resolve reads every row (ignores the high-water mark)
 constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load per record and column
 constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
+constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 

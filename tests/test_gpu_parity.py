@@ -1062,3 +1062,15 @@ def test_high_water_mark_reserve_relayout_remap(gpu_device):
     merge(cap1)
     check("remap")
     t.close()
+
+
+@pytest.mark.parametrize("form_off", ["0", "131072"])
+def test_two_rank_routing_kernel_forms(gpu_device, monkeypatch, form_off):
+    """The routing kernels in both forms (vector loads + wave-aggregated slots, and the strided
+    one-atomic-per-record form, CRDT_SORTED_FORM bit 131072): 2 ranks over the gloo table, the
+    packed wire into the sorted receivers and the 20-B wire into the gather path, vs the oracle."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
+    kw = dict(seed=83, R=70, per_cs=3000, n_local=30_000, n_new=20_000, millis_span=8, counter_span=4,
+              n_ranks=71, tomb_frac=0.1)
+    run_shard_gpu(kw, 2, "routed", path="sorted", counts=False)
+    run_shard_gpu(dict(CASE_SPECS)["drift_late"], 2, "routed")
