@@ -2168,7 +2168,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                     pf, c->d_misc);
             k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
-            if (c->form_off & kFormNoWholeLines)
+            if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
+                k_resolve_packed<false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc);
+            else if (c->form_off & kFormNoWholeLines)
                 k_resolve_packed<false, false><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);

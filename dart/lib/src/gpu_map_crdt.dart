@@ -78,6 +78,25 @@ class _ValueStore<V> {
     _free.add(h);
   }
 
+  /// Handles in use (the store's live size).
+  int get length => _values.length - _free.length;
+
+  /// Frees every handle not in [live] (the value handles the device table still holds) and
+  /// rebuilds the free list: bulk merges keep every stored handle, losers included.
+  void compact(Iterable<int> live) {
+    final keep = List<bool>.filled(_values.length, false);
+    for (final h in live) {
+      if (h != crdtNullValue && h < keep.length) keep[h] = true;
+    }
+    _free.clear();
+    for (var h = 0; h < _values.length; ++h) {
+      if (!keep[h]) {
+        _values[h] = null;
+        _free.add(h);
+      }
+    }
+  }
+
   void clear() {
     _values.clear();
     _free.clear();
@@ -239,6 +258,26 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
       calloc.free(mod);
     }
     if (notify) items.forEach((k, r) => _controller.add(MapEntry(k, r.value)));
+    _maybeCompact();
+  }
+
+  /// Mirrors MapCrdt._maybe_compact (crdt_amd/crdt.py): once the value store holds more than
+  /// twice as many handles as there are keys, the handles still referenced by the table are
+  /// read back (crdt_read_rows of every key id) and every other handle is freed.
+  void _maybeCompact() {
+    final nKeys = _keys.length;
+    if (_values.length <= 2 * (nKeys > 4096 ? nKeys : 4096)) return;
+    final ids = calloc<Uint32>(nKeys == 0 ? 1 : nKeys), val = calloc<Uint32>(nKeys == 0 ? 1 : nKeys);
+    try {
+      for (var i = 0; i < nKeys; ++i) {
+        ids[i] = i;
+      }
+      _check(_lib.readRows(_c, ids, nKeys, nullptr, nullptr, val, nullptr, crdtMemHost), 'crdt_read_rows');
+      _values.compact(val.asTypedList(nKeys == 0 ? 1 : nKeys).take(nKeys));
+    } finally {
+      calloc.free(ids);
+      calloc.free(val);
+    }
   }
 
   // --------------------------------------------------------------------------- SPI
@@ -381,6 +420,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
       calloc.free(res);
     }
     values.forEach((k, v) => _controller.add(MapEntry(k, v)));
+    _maybeCompact();
   }
 
   // ------------------------------------------------------------------------ merge
@@ -442,14 +482,23 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
         ..nChangesets = R
         ..mem = crdtMemHost;
       final st = _lib.merge(_c, batch, DateTime.now().millisecondsSinceEpoch, winners ? flags : nullptr, res);
-      _check(st, 'crdt_merge');
+      if (st < 0) {
+        // the library refused the call (nothing stored on a single context, crdt_merge.h): forget
+        // the keys and value handles this batch interned, as MapCrdt.mergeAll does (crdt.py)
+        _truncateKeys(newIdStart[0]);
+        for (var x = 0; x < n; ++x) {
+          _values.release(val[x]);
+        }
+        _check(st, 'crdt_merge');
+      }
       final stop = res.ref.nStored;
       _truncateKeys(newIdStart[stop]); // keys first seen in changesets never stored
       final storedEnd = offsets[stop];
       if (!winners) {                  // bulk form: no per-record outcome; the stored changesets'
-        for (var x = storedEnd; x < n; ++x) {   // handles stay referenced (losers unknown), the
-          _values.release(val[x]);              // unstored ones are released
+        for (var x = storedEnd; x < n; ++x) {   // handles stay referenced (losers unknown until
+          _values.release(val[x]);              // the next compaction), the unstored ones are released
         }
+        _maybeCompact();
         _rethrow(res);
         return;
       }
@@ -473,6 +522,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
           _controller.add(MapEntry(k, r.value)); // map_crdt.dart:36-38
         });
       }
+      _maybeCompact();
       _rethrow(res); // after the partial state is committed, like the reference
     } finally {
       calloc.free(kid);

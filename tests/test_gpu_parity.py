@@ -707,6 +707,30 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
 
 
+def _cold_bucket_case(seed):
+    """Keys spread over the whole of a > 2^20-key table: ~260 cold 4096-key buckets of a few
+    hundred records each (no bucket near the 65,536-record split), so every resolve runs the
+    unsplit-bucket kernels — the _frame_edge_case keys all sit in bucket 0, which is split."""
+    case = make_case(seed=seed, R=24, per_cs=4000, n_local=700_000, n_new=360_000, millis_span=4,
+                     counter_span=3, n_ranks=9, tomb_frac=0.15, neg_mod_frac=0.02)
+    assert case["n_ids"] > (1 << 20)
+    return case
+
+
+@pytest.mark.parametrize("form_off", ["0", "64", "128", "256", "448", "512", "1024", "2048", "8192", "32768",
+                                      "65536"])
+def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_off):
+    """Every CRDT_SORTED_FORM switch on records spread over many cold buckets, two levels: the
+    unsplit-bucket resolve of each form (the changed-rows-only writes with 13-B final records
+    among them) against the oracle."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
+    case = _cold_bucket_case(131)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=case["n_ids"],
+                              rank_bound=int(case["rank"].max()) + 1, device_cols=True)
+    assert res["plan"]["packed"] and res["plan"]["two_level"], res["plan"]
+    assert res["plan"]["key8"] == (form_off not in ("128", "448")), res["plan"]
+
+
 @pytest.mark.parametrize("L", [42, 43, 44, 45])
 def test_sorted_key8_frame_boundary(gpu_device, L):
     """The 1-B key column needs 4 free bits above the packed key (L + K + 13 <= 60, L / K the lt /
