@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--no-presharded", action="store_true", help="N > 1: skip the pre-sharded figure")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of each CPU baseline sample")
     p.add_argument("--cpu-changesets", type=int, default=64, help="changesets of the faithful CPU port's sample")
+    p.add_argument("--no-cpu-copy16", action="store_true",
+                   help="skip cpu_baseline_copy16 (the faithful port with its map copy on 16 threads)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
@@ -349,32 +351,57 @@ def main():
                 "value": 30.4e9, "unit": "records/s", "achieved": round(rate, 1), "frac": round(rate / 30.4e9, 3),
                 "source": "profiles/r01_ubench_rowwrite.txt"}
     elif path == "sorted" and apply_ms > 0:
-        # the level-1 partition scatter (one launch per step, HIP events around it): reads every
-        # applied record's 20 B, writes its partition record (packed 12 B + key column, or 16 + 4 B)
+        # the level-1 partition scatter (one launch per step, HIP events around it).  Contract bytes
+        # (SURVEY 8(d)): the 20 B of every record it reads; its partition record (packed 12 B + key
+        # column, or 16 + 4 B) is scratch, reported separately with the PMC traffic of the kernel
         out_b = (12 + 2) if plan["key16"] else (12 + 4) if plan["packed"] else (16 + 4)
         p1_us = tsum.get("part1_ms", 0.0) * 1e3 / K
-        n_app = int(offs[-1]) if world == 1 else None
+        n_app = int(tsum.get("part1_records", 0)) // max(K, 1)
         dk = {"kernel": "k_part_scatter1 (level-1 partition, one launch per step)",
               "phases_ms_per_step": {k: round(tsum.get(f"{k}_ms", 0.0) / K, 3)
                                      for k in ("scan", "part1", "part2", "resolve")},
               "apply_ms_per_step": round(apply_ms / K, 3), "plan": plan}
         if p1_us > 0 and n_app:
-            kb = n_app * (20 + out_b)
+            kb = n_app * 20
             dk.update({"avg_launch_us": round(p1_us, 1), "alg_bytes_per_launch": kb,
-                       "bytes_per_record": f"20 read + {out_b} written",
+                       "records_per_launch": n_app,
+                       "bytes_per_record": f"20 read (SURVEY 8(d)); + {out_b} B scratch written, not counted",
                        "achieved_GBs": round(kb / (p1_us / 1e6) / 1e9, 1),
                        "frac": round(kb / (p1_us / 1e6) / HBM_PEAK, 4)})
+            pk = pmc_kernel(args, path, "k_part_scatter1", world)
+            if pk:
+                tb = pk["read_bytes_per_step"] + pk["write_bytes_per_step"]
+                dk.update({"actual_traffic_bytes": int(tb), "actual_traffic_source": pk["source"],
+                           "actual_traffic_frac": round(tb / (p1_us / 1e6) / HBM_PEAK, 4)})
         roofline["dominant_kernel"] = dk
     # traffic: HBM bytes per step from this round's rocprofv3 --pmc passes of this exact command
-    if os.path.exists(PMC_FILE) and args.config == "fanin" and world == 1:
-        try:
-            pm = json.load(open(PMC_FILE))
-            if pm.get("command_args") == pmc_args(args) and pm.get("merge_path") == path:
-                roofline["traffic"] = pm["hbm_bytes_per_step"]
-                roofline["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
-        except Exception:  # noqa: BLE001
-            pass
+    pm = pmc_profile(args, path, world)
+    if pm:
+        roofline["traffic"] = pm["hbm_bytes_per_step"]
+        roofline["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
 
+    cpu = cpu16 = cpu_omp = parity = None
+    if world > 1 and args.config == "fanin" and not args.no_cpu:
+        # N > 1: every rank digests its shard (one 64-bit word per 2^20 slots, after the timed path's
+        # last merge); rank 0 regenerates the same batch unsharded, times the CPU baselines on it and
+        # runs the OpenMP oracle over all of it, then compares every shard's digests and the
+        # canonical with the oracle's state (the other ranks wait at the barrier)
+        dig = shard_digests(table, wl["capacity"])
+        mine = (rank, dig.tolist(), int(table.canonical))
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        if rank == 0:
+            full = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                             device=dev, order=args.order)
+            cpu = cpu_baseline(full, args.cpu_seconds, args.cpu_changesets, threads=1)
+            if not args.no_cpu_copy16:
+                cpu16 = cpu_baseline(full, args.cpu_seconds, args.cpu_changesets)
+            cpu_omp, _, oracle = cpu_baseline_omp(full, args.cpu_seconds, keep=True)
+            del full
+            torch.cuda.empty_cache()
+            parity = shard_parity(oracle, got, world) if oracle is not None else None
+            del oracle
+        barrier()
     # ---- pre-sharded figure (N > 1): every rank already holds exactly what it owns
     presharded = None
     if world > 1 and args.config == "fanin" and not args.no_presharded:
@@ -397,14 +424,18 @@ def main():
                               "exchange, only the clock collectives"}
         table.set_presharded(False)
 
-    # ---- CPU baselines (rank 0, N = 1): the C restatement of the reference algorithm
-    cpu = cpu_omp = parity = None
+    # ---- CPU baselines (rank 0, N = 1): the C restatement of the reference algorithm.
+    # cpu_baseline: the faithful port on ONE thread (the reference is a single Dart isolate: its
+    # recordMap() copy, clock reads, recv and winner loops all run on one core); cpu_baseline_copy16:
+    # the same with only the map copy spread over 16 threads; cpu_baseline_omp: the optimised port
     if rank == 0 and world == 1 and not args.no_cpu:
         if job:                        # the census merged with win flags: redo the timed path's merge
             reset()
             step()
             torch.cuda.synchronize()
-        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_changesets)
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_changesets, threads=1)
+        if not args.no_cpu_copy16:
+            cpu16 = cpu_baseline(wl, args.cpu_seconds, args.cpu_changesets)
         cpu_omp, parity = cpu_baseline_omp(wl, args.cpu_seconds, table)
     pcie = None
     if rank == 0 and world == 1 and not args.no_pcie and not wl.get("per_call"):
@@ -420,7 +451,8 @@ def main():
                    "parallelism": f"keyshard{n}-routed" if world > 1 else "single", "merge_path": path,
                    "row_bytes": row_bytes,
                    "step_ms_all": [round(x, 3) for x in step_ms]},
-        "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_omp": cpu_omp, "parity": parity,
+        "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
+        "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
         "pcie_inclusive": pcie, "presharded": presharded,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),
@@ -439,21 +471,48 @@ def main():
         dist.destroy_process_group()
 
 
+def pmc_profile(args, path, world):
+    """The committed rocprofv3 --pmc summary (PMC_FILE) when it was taken on this exact command."""
+    if not os.path.exists(PMC_FILE) or args.config != "fanin" or world != 1:
+        return None
+    try:
+        pm = json.load(open(PMC_FILE))
+    except Exception:  # noqa: BLE001
+        return None
+    if pm.get("command_args") != pmc_args(args) or pm.get("merge_path") != path:
+        return None
+    return pm
+
+
+def pmc_kernel(args, path, name, world):
+    """Per-step HBM bytes of the kernel whose name starts with ``name`` in the PMC summary."""
+    pm = pmc_profile(args, path, world)
+    if not pm:
+        return None
+    for k, v in pm.get("kernels", {}).items():
+        if k.startswith(name + "<") or k == name:
+            return dict(v, source=os.path.relpath(PMC_FILE, ROOT) + f" [{k}]")
+    return None
+
+
 def pmc_args(args) -> list:
     """The arguments that define the workload a committed PMC profile must match."""
     return [args.config, args.records, args.replicas, args.keys, args.local, args.zipf, args.order, args.path,
             bool(args.exact_counts)]
 
 
-def cpu_baseline(wl, budget_s, n_changesets=64):
+def cpu_baseline(wl, budget_s, n_changesets=64, threads=None):
     """Times oracle/merge_oracle.c in faithful mode — the reference algorithm: a full recordMap()
-    copy of the map per merge (map_crdt.dart:43, on T threads: the only unordered part), the
-    recv loop with a clock read per record (hlc.dart:82) and the winner loop, sequential — on the
-    first ``n_changesets`` changesets of the same workload (stopping early past ~budget_s x 4),
-    in blocks of 8 changesets whose rates give the spread."""
+    copy of the map per merge (map_crdt.dart:43, on ``threads`` threads: the only unordered part),
+    the recv loop with a clock read per record (hlc.dart:82) and the winner loop, sequential — on the
+    first ``n_changesets`` changesets of the same workload (stopping early past ~budget_s x 4,
+    threads=1: past ~budget_s), in blocks of changesets whose rates give the spread."""
     import torch
     from oracle.oracle_c import OracleTable
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    block = 8 if threads > 1 else 2
+    limit = 4 * budget_s if threads > 1 else budget_s
     loc = wl["local"]
     cap = wl["capacity"]
     t = OracleTable(cap, 0, wl["c0"])
@@ -464,8 +523,8 @@ def cpu_baseline(wl, budget_s, n_changesets=64):
     own = wl["owned"]
     want = min(n_changesets, wl["R"])
     done, recs, el, blocks = 0, 0, 0.0, []
-    while done < want and el < 4 * budget_s:
-        j1 = min(done + 8, want)
+    while done < want and el < limit:
+        j1 = min(done + block, want)
         b, e = int(offs[done]), int(offs[j1])
         cols = [own[k][b:e].cpu().numpy() for k in ("key", "lt", "rank", "val")]
         sub = (offs[done:j1 + 1] - offs[done]).astype(np.uint64)
@@ -483,14 +542,15 @@ def cpu_baseline(wl, budget_s, n_changesets=64):
     torch.cuda.synchronize()
     return {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
             "spread": {"min": round(min(blocks), 1), "median": round(float(np.median(blocks)), 1),
-                       "max": round(max(blocks), 1), "blocks": len(blocks), "changesets_per_block": 8},
+                       "max": round(max(blocks), 1), "blocks": len(blocks), "changesets_per_block": block},
             "sample": f"first {done} of {wl['R']} changesets ({recs:,} records, {100 * recs / wl['total']:.1f} % of "
                       f"the batch) merged into the full {cap:,}-row map by oracle/merge_oracle.c in faithful "
-                      f"mode: one full map copy per merge (map_crdt.dart:43) on {threads} threads, one clock "
-                      f"read per record (hlc.dart:82) and the recv / winner loops on one thread, {el:.1f}s"}
+                      f"mode: one full map copy per merge (map_crdt.dart:43) on {threads} thread"
+                      f"{'s' if threads > 1 else ''}, one clock read per record (hlc.dart:82) and the recv / "
+                      f"winner loops on one thread, {el:.1f}s; host nproc {os.cpu_count()}"}
 
 
-def cpu_baseline_omp(wl, budget_s, table=None):
+def cpu_baseline_omp(wl, budget_s, table=None, keep=False):
     """Times oracle/merge_omp.c (the optimised multi-core merge, same results) on the leading
     changesets of the same workload, 16 changesets per call, within ~budget_s seconds.
 
@@ -525,12 +585,16 @@ def cpu_baseline_omp(wl, budget_s, table=None):
     parity = None
     if table is not None and done == wl["R"]:
         parity = full_parity(table, t, wl["capacity"])
+    kept = t if keep and done == wl["R"] else None
     del t
     torch.cuda.synchronize()
-    return ({"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
-             "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
-                       f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
-                       f"{threads} OpenMP threads, {el:.1f}s"}, parity)
+    base = {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
+                      f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
+                      f"{threads} OpenMP threads, {el:.1f}s"}
+    if keep:
+        return base, parity, kept
+    return base, parity
 
 
 def host_input_rate(table, wl, reset, max_records: int = 128 << 20) -> dict:
@@ -563,6 +627,63 @@ def host_input_rate(table, wl, reset, max_records: int = 128 << 20) -> dict:
     out["sample"] = (f"first {j1} of {wl['R']} changesets ({n:,} records, {20 * n / 1e9:.2f} GB of columns) "
                      f"merged from host buffers: crdt_merge copies them to HBM, then runs the same path")
     return out
+
+
+DIGEST_BLOCK = 1 << 20          # slots per parity digest word
+_DIG_P = [np.uint64(x) for x in (0x9E3779B97F4A7C15, 0xC2B2AE3D27D4EB4F, 0x165667B19E3779F9,
+                                 0xD6E8FEB86659FD93, 0xFF51AFD7ED558CCD)]
+
+
+def row_digests(lt, rank, val, mod, slot0: int) -> np.ndarray:
+    """One 64-bit word per DIGEST_BLOCK slots (slot0 a multiple of it): the wrapping sum over the
+    block of a mix of (slot, lt, rank, val, mod) — equal blocks give equal words, and a row that
+    differs in any field (or sits at another slot) changes its block's word."""
+    n = len(lt)
+    with np.errstate(over="ignore"):
+        slot = np.arange(slot0, slot0 + n, dtype=np.uint64)
+        rv = (np.asarray(rank).astype(np.uint64) << np.uint64(32)) | np.asarray(val).astype(np.uint64)
+        h = (np.asarray(lt).view(np.uint64) * _DIG_P[0]) ^ (np.asarray(mod).view(np.uint64) * _DIG_P[1])
+        h ^= rv * _DIG_P[2]
+        h ^= slot * _DIG_P[3]
+        h ^= h >> np.uint64(29)
+        h *= _DIG_P[4]
+        h ^= h >> np.uint64(32)
+    starts = np.arange(0, n, DIGEST_BLOCK)
+    return np.add.reduceat(h, starts) if n else np.zeros(0, np.uint64)
+
+
+def shard_digests(table, cap: int, chunk: int = 1 << 25) -> np.ndarray:
+    """row_digests of this rank's table, slots [0, cap)."""
+    out = []
+    for b in range(0, cap, chunk):
+        e = min(b + chunk, cap)
+        lt, rk, val, mod = table.read_rows(np.arange(b, e, dtype=np.uint32))
+        out.append(row_digests(lt, rk, val, mod, b))
+    return np.concatenate(out) if out else np.zeros(0, np.uint64)
+
+
+def shard_parity(oracle, got, world: int) -> dict:
+    """Every rank's shard digests (``got``: (rank, digests, canonical) per rank) against the same
+    digests of the oracle's rows key % world == rank at slot key // world."""
+    from oracle.oracle_c import new_table
+    ts = time.perf_counter()
+    K = len(oracle.rows)
+    bad_blocks, canon_bad, blocks = 0, 0, 0
+    for r, dig, canon in got:
+        sh = oracle.rows[r::world]
+        cap = len(dig) and -(-K // world)
+        if len(sh) < cap:                              # slots past the last key: never-written fill
+            sh = np.concatenate([sh, new_table(cap - len(sh))])
+        want = row_digests(sh["lt"], sh["rank"], sh["val"], sh["mod"], 0)
+        d = np.asarray(dig, np.uint64)
+        blocks += len(want)
+        bad_blocks += int(np.count_nonzero(d != want)) if len(d) == len(want) else len(want)
+        canon_bad += int(canon != oracle.canonical)
+    return {"rows": K, "shards": world, "digest_blocks": blocks, "blocks_differing": bad_blocks,
+            "canonical_equal": canon_bad == 0, "equal": bad_blocks == 0 and canon_bad == 0,
+            "against": "oracle/merge_omp.c final state of the unsharded batch, per-shard digests "
+                       f"(one 64-bit word per {DIGEST_BLOCK} slots: bench.row_digests)",
+            "seconds": round(time.perf_counter() - ts, 1)}
 
 
 def full_parity(table, oracle, cap: int, chunk: int = 1 << 25) -> dict:

@@ -120,7 +120,8 @@ struct Misc {
     uint32_t err;          // key range violation
     uint32_t vdone;        // k_verify<true> workgroups finished (the last one resolves)
     uint32_t tiles_hot;    // scan tiles holding a record above C_0, every kHotSample-th (next scan's form)
-    uint32_t pad;
+    uint32_t miss;         // anchored frame (sorted_path.inc): max of ~j over the changesets j holding a
+                           // record below the frame (0: none) — the frame is invalid if one is applied
     crdt_result result;    // filled by k_resolve
     // frame of the batch's records (k_scan<*, *, true>) for the sorted path's packed key
     // (sorted_path.inc), as max-accumulators whose identity is the memset's 0:
@@ -593,8 +594,11 @@ __global__ __launch_bounds__(64) void k_verify(
     long long* __restrict__ cand_key, int64_t* __restrict__ cand_P,
     uint32_t* __restrict__ cand_kind, int64_t* __restrict__ cand_ms,
     const long long* __restrict__ pbase, const unsigned long long* __restrict__ ibase,
-    long long* __restrict__ event, int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj)
+    long long* __restrict__ event, int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
+    uint32_t tile_recs)
 {
+    // tile_recs: records per tile of T / tstart / cand_tile (kTile for the scan's tiles, kPTile for the
+    // level-1 partition tiles of the anchored sorted path, whose scatter reduces the tile maxima).
     // pbase / ibase (optional): this ctx holds only a PART of changeset j, preceded in
     // its iteration order by records of other ranks whose max lt is pbase[j] and whose
     // count is ibase[j] (key-sharded "parts" protocol, crdt_amd/dist.py).
@@ -613,8 +617,8 @@ __global__ __launch_bounds__(64) void k_verify(
         if (pbase) P = imax(P, (int64_t)pbase[j]);
         for (uint32_t u = tstart[j] + lane; u < gt; u += 64) P = imax(P, T[u]);
         P = wave_max(P);
-        const uint64_t base = offs[j] + (uint64_t)t * kTile;
-        const uint64_t end = std::min<uint64_t>(base + kTile, offs[j + 1]);
+        const uint64_t base = offs[j] + (uint64_t)t * tile_recs;
+        const uint64_t end = std::min<uint64_t>(base + tile_recs, offs[j + 1]);
         bool found = false;
         uint64_t fi = 0;
         int64_t fp = 0, fms = 0;
@@ -1320,6 +1324,7 @@ constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load 
 constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
 constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
+constexpr uint32_t kFormNoAnchor = 262144;   // the anchored sorted path off: the scan pass and the scan's frame
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1366,6 +1371,7 @@ struct crdt_ctx {
     std::vector<hipEvent_t> events;
     std::vector<uint32_t> windows;  // launches of each timed apply window (events ev_window(k, *))
     bool sorted_phases = false;     // events ev_window(1..3, *) bracket the sorted path's phases
+    uint64_t p1_records = 0;        // records of the first window's level-1 scatter (crdt_timing)
     uint32_t apply_total = 0;
     // sorted path (sorted_path.inc): 0 = auto, 1 = always gather (K2), 2 = sorted when allowed
     int merge_path = 0;
@@ -1408,6 +1414,10 @@ struct crdt_ctx {
     const uint32_t* hist1_key = nullptr;
     uint32_t hist1_shift = 0;
     bool last_packed = false;       // the last sorted apply used the packed form
+    bool anchored = false;          // this call runs the anchored sorted path (merge_anchored)
+    bool last_wire_pk = false;      // the last sharded merge routed 16-B packed records
+    bool last_anchored = false;
+    uint32_t anchor_skip = 0;       // calls left before the anchored frame is tried again after a miss
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
     bool last_hw = false;           // ... whose packed resolve skipped the rows >= hw_read
@@ -1562,6 +1572,9 @@ inline size_t events_for(size_t nsegs) {     // (windows 1..3 also bracket the s
     return std::max(ev_window(nsegs / kTimingStride + 2, true), ev_window(3, true)) + 1;
 }
 
+// finish_apply: the anchored frame missed (a record below it in an applied changeset); internal
+constexpr int kAnchorRetry = 1000;
+
 inline void raise_hw(crdt_ctx* c, uint64_t key_end) {
     c->hw = std::max<uint64_t>(c->hw, std::min<uint64_t>(key_end, c->cap));
 }
@@ -1687,7 +1700,7 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
         k_verify<true><<<kVerifyBlocks, 64, 0, c->stream>>>(
             cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, R, c->d_T.p, c->d_Cprev.p, wall,
             c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
-            c->d_candms.p, d_pbase, d_ibase, d_event, c->canonical, c->d_Rj.p, c->d_Cj.p);
+            c->d_candms.p, d_pbase, d_ibase, d_event, c->canonical, c->d_Rj.p, c->d_Cj.p, (uint32_t)kTile);
         c->resolved = true;                                   // misc->stop / result are set
         HIPCHK(hipGetLastError());
         return CRDT_OK;
@@ -1698,7 +1711,7 @@ int phase_clock(crdt_ctx* c, const crdt_batch* home, int64_t wall, const long lo
         k_verify<false><<<kVerifyBlocks, 64, 0, c->stream>>>(
             cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, R, c->d_T.p, c->d_Cprev.p, wall,
             c->local_rank, c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
-            c->d_candms.p, d_pbase, d_ibase, d_event, 0, nullptr, nullptr);
+            c->d_candms.p, d_pbase, d_ibase, d_event, 0, nullptr, nullptr, (uint32_t)kTile);
     HIPCHK(hipGetLastError());
     return CRDT_OK;
 }
@@ -1775,6 +1788,8 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     if (host_flags && n) HIPCHK(hipMemcpyAsync(host_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->anchored && c->h_misc->miss != 0 && 0xFFFFFFFFu - c->h_misc->miss < c->h_misc->stop)
+        return kAnchorRetry;                    // nothing stored, canonical untouched: rerun exactly
     crdt_result res = c->h_misc->result;
     c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
     if (c->key_end_valid && !c->has_comm)        // rows stored lie in the sorted path's buckets
@@ -1931,13 +1946,16 @@ void prof_resolve_report() {
 // window of kWindow changesets a level-1 (+ level-2) partition of the applied records and
 // the per-bucket LDS resolve.  sg = the batch's changeset segments (host), in changeset
 // order; one changeset may be several segments (records routed in from several ranks).
+// anchor (merge_anchored): the packed form on the frame given, one window, and the clock phase
+// (tile maxima from the level-1 scatter, recurrence, exception scan, stop point) run between the
+// level-1 scatter and level 2 instead of before this function.
 int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
-                 crdt_result* out) {
+                 crdt_result* out, const PackFrame* anchor = nullptr) {
     const uint32_t R = c->plan_R;
-    if (!c->resolved)
+    if (!c->resolved && !anchor)
         k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     c->resolved = false;
-    ev_record(c, kEvApply);
+    if (!anchor) ev_record(c, kEvApply);
     c->windows.clear();
     c->apply_total = 1;
     if (c->timing) ev_record(c, ev_window(0, false));
@@ -1948,7 +1966,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     // batch fits the 64-bit key (one read-back of Misc per call), else wide payloads + lists
     PackFrame pf{};
     bool pk = false;
-    if (cols.packed_in || (!c->counts && c->packed_resolve && c->frame_on)) {
+    if (anchor) {
+        pf = *anchor;
+        pk = true;
+    } else if (cols.packed_in || (!c->counts && c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         pf = frame_of(c);
@@ -2031,48 +2052,77 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
         // level-1 histogram: counted by the scan (then only the changesets >= stop are cleared)
         // or here
-        const bool h1 = c->hist1_fused && s0 == 0 && se == ns_all && !cols.packed_in && cols.key == c->hist1_key &&
-                        c->hist1_shift == shift1 && nt1 == c->plan_ptiles;
+        const bool h1 = !anchor && c->hist1_fused && s0 == 0 && se == ns_all && !cols.packed_in &&
+                        cols.key == c->hist1_key && c->hist1_shift == shift1 && nt1 == c->plan_ptiles;
         const uint32_t* hist1 = h1 ? c->p_hist1.p : c->p_hist.p;
         if (h1)
             k_hist_trim<<<256, 256, 0, c->stream>>>(c->p_hist1.p, c->d_ptb, R, c->d_misc);
-        else
-            k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc, c->cap, shift1,
-                                                                 c->p_hist.p);
+        else                                        // (anchored: every changeset, stop not known yet)
+            k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, anchor ? nullptr : c->d_misc,
+                                                                 c->cap, shift1, c->p_hist.p);
         c->last_hist1_fused = h1;
         k_scan_part<<<nc1, 256, 0, c->stream>>>(hist1, sm1, c->p_part.p);
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
         const bool ph = c->timing && s0 == 0;       // phase events: the first window
+        if (anchor) ev_record(c, kEvScan);          // (anchored: the keys-only histogram pass and its scans)
         if (ph) ev_record(c, ev_window(1, false));
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
-        if (cols.packed_in && k16)
+        const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
+        const AnchorArgs an{c->d_T.p, c->d_candtile.p, wsub(imax(c->canonical, wp), pf.lt0), c->local_rank};
+        if (anchor && k16)
+            k_part_scatter1<true, false, true, kL1AnchorItems, true, true, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, an);
+        else if (anchor)
+            k_part_scatter1<true, false, false, kL1AnchorItems, true, false, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, an);
+        else if (cols.packed_in && k16)
             k_part_scatter1<true, true, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         else if (cols.packed_in)
             k_part_scatter1<true, true, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         else if (k16 && !(c->form_off & kFormNoVecLoads))
             k_part_scatter1<true, false, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         else if (k16)
             k_part_scatter1<true, false, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         else if (pk)
             k_part_scatter1<true, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         else
             k_part_scatter1<false, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         if (ph) ev_record(c, ev_window(1, true));
+        if (anchor) {
+            // the clock phase on the scatter's tile maxima (level-1 tiles of kPTile records): M_j,
+            // the recurrence, the exact exception scan of candidate tiles, stop point and canonical
+            k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_ptb, R, c->d_M.p);
+            k_clock<false><<<1, 1024, 0, c->stream>>>(c->d_M.p, nullptr, nullptr, R, wall, c->canonical,
+                                                      c->d_Cprev.p, c->d_Rj.p, c->d_Cj.p, c->d_event.p);
+            k_verify<false><<<kVerifyBlocks, 64, 0, c->stream>>>(
+                cols.lt, cols.rank, nullptr, c->d_offs, c->d_ptb, R, c->d_T.p, c->d_Cprev.p, wall, c->local_rank,
+                c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p, c->d_candms.p, nullptr,
+                nullptr, c->d_event.p, 0, nullptr, nullptr, (uint32_t)kPTile);
+            k_resolve_local<<<1, 256, 0, c->stream>>>(c->d_misc, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
+                                                      c->d_candms.p, c->d_event.p);
+            k_resolve<<<1, 64, 0, c->stream>>>(c->d_event.p, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+            ev_record(c, kEvClock);
+            ev_record(c, kEvApply);
+        }
         if (ph) ev_record(c, ev_window(2, false));
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
@@ -2197,6 +2247,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (ph) {
             ev_record(c, ev_window(3, true));
             c->sorted_phases = true;
+            c->p1_records = nw;
         }
         HIPCHK(hipGetLastError());
         // the next window reads rows this one may have written anywhere below the capacity
@@ -2260,6 +2311,73 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     return apply_segs(c, cols, owned->offsets[R], owned->mem, wall, d_event, win_flags, out, allow_sorted);
 }
 
+// ---- the anchored sorted path ----------------------------------------------------------------
+// Every record a call applies has lt <= max(C_0, ((wall + 60000) << 16) | 0xFFFF) + R: recv() accepts a
+// record above the running canonical only if its millis is within 60 s of the wall clock
+// (hlc.dart:85-94; no explicit millis column, so millis = lt >> 16), and each send() adds at most one
+// (hlc.dart:58-73; by induction over the changesets).  So the packed key's lt frame can
+// be fixed before any record is read: the 2^L - 1 values up to that anchor, L = 60 - K - 13 (13-B
+// final records, K = the bits of the declared rank bound).  The clock scan's work (tile maxima,
+// candidate tiles) then rides on the level-1 scatter's own loads — no pass reads lt alone, and the
+// host does not wait for a frame — leaving a keys-only level-1 histogram as the one pre-pass.  A
+// record below the frame in an applied changeset (a replica further behind than the frame reaches)
+// makes the call store nothing (Misc::miss); the host reruns it on the scan's exact frame and leaves
+// the anchor off for the next calls of this ctx.
+bool anchored_frame(const crdt_ctx* c, uint32_t R, int64_t wall, PackFrame* out) {
+    if (!c->rank_bound) return false;
+    const uint64_t r1 = c->rank_bound;                   // rank fields 0 .. bound - 1, bound = clamp
+    int K = 0;
+    while (K < 64 && (r1 >> K) != 0) ++K;
+    const int L = 60 - (K + 13);
+    if (L < 30) return false;                            // under ~16 s of millis: not worth a miss
+    const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
+    const int64_t b = imax(c->canonical, wp);
+    if (b > INT64_MAX - (int64_t)R - 1) return false;
+    const int64_t top = b + (int64_t)R;
+    PackFrame f;
+    f.lt_span = (1ull << L) - 2;                         // span + 1 has L bits (make_frame's rule)
+    f.lt0 = (int64_t)((uint64_t)top - f.lt_span);
+    f.rk0 = 0;
+    f.rk_span = c->rank_bound - 1;
+    f.sh = (uint32_t)(K + 13);
+    f.rk_mask = (1ull << K) - 1;
+    f.rk_limit = c->rank_bound;
+    f.ok = true;
+    f.key4 = true;
+    *out = f;
+    return true;
+}
+
+// One anchored crdt_merge of resident columns (no millis column, one window of changesets); returns
+// kAnchorRetry when the frame missed (nothing stored, canonical untouched).
+int merge_anchored(crdt_ctx* c, const crdt_batch* b, int64_t wall, const PackFrame& pf, crdt_result* out) {
+    c->fused = false;
+    c->resolved = false;
+    c->hist1_fused = false;
+    const uint32_t R = b->n_changesets;
+    uint64_t tiles = 0;
+    uint32_t mt = 0;
+    int st;
+    if ((st = upload_plan(c, b, &tiles, &mt))) return st;
+    const uint64_t pt = c->plan_ptiles + 1;              // level-1 tiles: T, candidate lists
+    HIPALLOC(c->d_T.ensure(pt)); HIPALLOC(c->d_candtile.ensure(pt)); HIPALLOC(c->d_candkey.ensure(pt));
+    HIPALLOC(c->d_candP.ensure(pt)); HIPALLOC(c->d_candkind.ensure(pt)); HIPALLOC(c->d_candms.ensure(pt));
+    HIPALLOC(c->d_Cprev.ensure(R + 1)); HIPALLOC(c->d_Rj.ensure(R + 1)); HIPALLOC(c->d_Cj.ensure(R + 1));
+    if ((st = reset_misc(c))) return st;
+    c->plan_R = R;
+    c->plan_tiles = tiles;
+    c->plan_mt = mt;
+    c->frame_on = true;
+    c->frame_lt_only = true;
+    Cols cols;
+    cols.key = b->key_id; cols.lt = b->lt; cols.rank = b->rank; cols.val = b->val;
+    c->anchored = true;
+    c->last_sorted = true;
+    st = apply_sorted(c, cols, c->segs, wall, c->d_event.p, out, &pf);
+    c->anchored = false;
+    return st;
+}
+
 void collect_timing(crdt_ctx* c) {
     crdt_timing t{};
     if (c->timing) {
@@ -2280,7 +2398,11 @@ void collect_timing(crdt_ctx* c) {
             t.part1_ms = el(ev_window(1, false), ev_window(1, true));
             t.part2_ms = el(ev_window(2, false), ev_window(2, true));
             t.resolve_ms = el(ev_window(3, false), ev_window(3, true));
+            t.part1_records = c->p1_records;
         }
+        // anchored: scan_ms = the keys-only level-1 histogram pass; the clock phase follows the level-1
+        // scatter, whose own time is part1_ms
+        if (c->last_anchored) t.clock_ms = std::max(0.0, t.clock_ms - t.part1_ms);
     }
     c->last_timing = t;
 }
@@ -2704,6 +2826,27 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     // the sorted path's packed form needs the records' frame: the scan reduces it on the way
     c->segs.from_offsets(batch->offsets, R);
     const bool frame = !c->counts && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
+    c->last_anchored = false;
+    PackFrame apf;
+    if (frame && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
+        !(c->form_off & kFormNoAnchor) && anchored_frame(c, R, wall, &apf)) {
+        if (c->anchor_skip) {
+            --c->anchor_skip;
+        } else {
+            ev_record(c, kEvStart);
+            st = merge_anchored(c, &dev, wall, apf, out);
+            if (st != kAnchorRetry) {
+                c->last_anchored = true;
+                if (c->timing) {
+                    ev_record(c, kEvEnd);
+                    hipStreamSynchronize(c->stream);
+                }
+                collect_timing(c);
+                return st;
+            }
+            c->anchor_skip = 16;        // this replica's peers reach below the anchor: exact frames for a while
+        }
+    }
     ev_record(c, kEvStart);
     if ((st = phase_scan(c, &dev, wall, c->d_M.p, true, frame, true, batch->mem == CRDT_MEM_DEVICE))) return st;
     ev_record(c, kEvScan);
@@ -2756,7 +2899,9 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_key8) f |= CRDT_PLAN_KEY8;
         if (c->last_key16) f |= CRDT_PLAN_KEY16;
         if (c->last_hw) f |= CRDT_PLAN_HIGH_WATER;
+        if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
     }
+    if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     *flags = f;
     return CRDT_OK;
 }

@@ -16,7 +16,8 @@
  *             String.compareTo (hlc.dart:160), so nodeId equality == rank equality;
  *   val     : uint32 value handle; CRDT_NULL_VALUE marks a tombstone
  *             (record.dart:17, isDeleted <=> value == null).
- * The device keeps one 32-byte row per key id: {lt, rank, val, mod, aux} where
+ * The device keeps one row per key id: {i64 lt; u32 rank; i32 mod_hi; u32 mod_lo; u32 val},
+ * 24 B apart by default (32 B with crdt_set_row_bytes: 8 zero bytes of padding), where
  * mod is Record.modified.logicalTime.  A row whose mod < 0 is invisible to
  * merge and to recordMap() (map_crdt.dart:42-45); never-written rows hold a
  * negative mod.
@@ -111,6 +112,7 @@ typedef struct crdt_timing {
     double part1_ms;
     double part2_ms;
     double resolve_ms;
+    uint64_t part1_records;    /* records the level-1 partition scatter read in that window */
 } crdt_timing;
 
 /* ---- lifecycle ------------------------------------------------------------ */
@@ -272,8 +274,13 @@ enum crdt_plan_flags {
     CRDT_PLAN_HIST_IN_SCAN = 8,  /* ... with its level-1 histogram counted by the scan */
     CRDT_PLAN_KEY8 = 16,         /* ... with 13-B final records (1-B key column, 4 key bits in the packed key) */
     CRDT_PLAN_KEY16 = 32,        /* ... and 14-B level-1 records (2-B key column) */
-    CRDT_PLAN_HIGH_WATER = 64    /* ... and its resolve did not read the rows at or above the table's
+    CRDT_PLAN_HIGH_WATER = 64,   /* ... and its resolve did not read the rows at or above the table's
                                     high-water mark of written rows (never-written fill) */
+    CRDT_PLAN_ANCHORED = 128,    /* ... on the anchored frame: the packed key's lt range fixed before any
+                                    record is read (every applied record is <= max(C_0, wall + 60 s) + R,
+                                    hlc.dart:92-94), the clock scan folded into the level-1 scatter */
+    CRDT_PLAN_WIRE_PACKED = 256  /* sharded ctx: records crossed the all-to-all as 16-B packed
+                                    {slot, (lt, rank, changeset) key, val} instead of 20 B */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

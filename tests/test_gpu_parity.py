@@ -3,7 +3,7 @@ and the C restatement, bit for bit — rows, win flags, canonical, exceptions.""
 import numpy as np
 import pytest
 
-from tests._cases import ABSENT_MOD, CASE_SPECS, NULL, make_case, oracle_run
+from tests._cases import ABSENT_MOD, CASE_SPECS, NULL, WALL, make_case, oracle_run
 from tests.test_golden_cpu import check_rows, golden_case
 
 pytestmark = pytest.mark.gpu
@@ -249,6 +249,24 @@ def _init_pg(dist, rank, world, backend):
         dist.init_process_group(backend, rank=rank, world_size=world)
 
 
+def _make_injected(kw):
+    """make_case(**kw) with an optional record that raises at (41, 123,456): kw["inject"] = "drift"
+    (millis past wall + 60 s) or "dup" (the local node id, above every clock the call reaches)."""
+    kw = dict(kw)
+    inject = kw.pop("inject", None)
+    case = make_case(**kw)
+    if inject:
+        x = int(case["offsets"][41]) + 123_456
+        case["lt"] = case["lt"].copy()
+        case["rank"] = case["rank"].copy()
+        if inject == "drift":
+            case["lt"][x] = (case["wall"] + 60_001) << 16
+        else:
+            case["lt"][x] = max(int(case["lt"].max()), case["c0"]) + 1000
+            case["rank"][x] = case["local_rank"]
+    return case
+
+
 def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path="gather", counts=True):
     """One rank of a sharded replica on cuda:0: the library's collective crdt_merge
     (comm_path.inc) over RCCL (backend nccl) or the host-staged gloo communicator."""
@@ -263,7 +281,7 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     _init_pg(dist, rank, world, backend)
     try:
-        case, sel, part_offs = layout(make_case(**case_kw), world, rank, kind)
+        case, sel, part_offs = layout(_make_injected(case_kw), world, rank, kind)
         cap = -(-case["n_ids"] // world)
         t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
         t.set_merge_path(path)
@@ -291,6 +309,7 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         res, _ = t.merge(dev(key.astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]),
                          dev(case["val"][sel]), part_offs, case["wall"], millis=millis, win_flags=flags)
         res["path"] = t.last_path()
+        res["plan"] = t.last_plan()
         lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
         fl = flags[:len(sel)].cpu().numpy() if path == "gather" else None
         q.put((rank, res, lt, rk, val, mod, sel, fl))
@@ -303,7 +322,7 @@ def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True):
     import torch.multiprocessing as mp
 
     from tests.test_dist_cpu import _free_port, layout
-    case, _, _ = layout(make_case(**kw), world, 0, kind)
+    case, _, _ = layout(_make_injected(kw), world, 0, kind)
     orows, ores, oflags = oracle_run(case)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -312,7 +331,7 @@ def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs = sorted([q.get(timeout=180) for _ in range(world)], key=lambda o: o[0])
+    outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -444,6 +463,32 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device):
             assert res[f] == ref[f], (rank, f)
         for a, b in zip(shard, rows):
             assert np.array_equal(a, b[rank::2]), rank
+
+
+@pytest.mark.parametrize("name", ["drift_late", "dup_node", "r8_tombstones"])
+def test_eight_rank_routed_small(gpu_device, name):
+    """G = 8 (route_bits(8), the 8-way count exchange, grouped all-to-all over 7 peers): the small
+    golden cases routed over 8 ranks on one GPU through the gloo communicator, sorted receivers in
+    the order-free form — rows of all 8 shards, canonical and exception fields vs the oracle."""
+    outs = run_shard_gpu(dict(CASE_SPECS)[name], 8, "routed", path="sorted", counts=False)
+    assert all(o[1]["path"] in ("sorted", "gather") for o in outs)
+
+
+@pytest.mark.parametrize("inject", [None, "drift", "dup"])
+def test_eight_rank_routed_packed_sorted(gpu_device, inject):
+    """The rehearsal of config 4's 8-GPU plan: 8 ranks on one GPU over the gloo communicator,
+    16M records in 64 changesets (replica j whole on rank j % 8, records routed to key % 8).  The
+    global frame fits, so records cross as 16-B packed wire records and every owner resolves them
+    on the sorted path; a drift or a duplicate-node record raises at (41, 123,456).  Every row of all
+    8 shards, the canonical clock, status and exception fields against the C oracle."""
+    kw = dict(seed=808, R=64, per_cs=250_000, n_local=1_500_000, n_new=600_000, millis_span=1 << 12,
+              counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
+    outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False)
+    for rank, res, *_ in outs:
+        assert res["path"] == "sorted" and res["plan"]["wire_packed"], (rank, res["plan"])
+        assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
+        if inject:
+            assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
 
 
 # ------------------------------------------------------------------ sorted path
@@ -631,6 +676,7 @@ def test_sorted_hist_in_scan(gpu_device, monkeypatch, kind, cap):
     """The level-1 histogram counted by the scan (device columns, rank bound, order-free form):
     same rows / result as the oracle and as the separate histogram pass (CRDT_HIST_FUSE=0),
     including a stop < R (rows of the unapplied changesets' tiles cleared) and one / two levels."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(NO_ANCHOR))     # the scan's path, not the anchored one
     if kind == "edges":
         case = _frame_edge_case(95)
     elif kind == "late_drift":
@@ -693,17 +739,22 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
     t.close()
 
 
+NO_ANCHOR = 262144        # CRDT_SORTED_FORM bit: the anchored sorted path off (the scan pass runs)
+
+
+@pytest.mark.parametrize("anchored", [True, False])
 @pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536"])
-def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
+def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off, anchored):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
     level-2 histogram with 2-B loads into shared bins, the level-1 scatter's / the scan's narrow
-    loads, 32K-record level-2 tiles) gives the same rows."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
+    loads, 32K-record level-2 tiles) gives the same rows, on the anchored path and the scan's."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (0 if anchored else NO_ANCHOR)))
     case = _frame_edge_case(99)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
+    assert res["plan"]["anchored"] == anchored, res["plan"]
     assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
 
 
@@ -717,18 +768,79 @@ def _cold_bucket_case(seed):
     return case
 
 
+@pytest.mark.parametrize("anchored", [True, False])
 @pytest.mark.parametrize("form_off", ["0", "64", "128", "256", "448", "512", "1024", "2048", "8192", "32768",
                                       "65536"])
-def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_off):
+def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_off, anchored):
     """Every CRDT_SORTED_FORM switch on records spread over many cold buckets, two levels: the
     unsplit-bucket resolve of each form (the changed-rows-only writes with 13-B final records
-    among them) against the oracle."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
+    among them) against the oracle, anchored and not."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (0 if anchored else NO_ANCHOR)))
     case = _cold_bucket_case(131)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=case["n_ids"],
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"], res["plan"]
     assert res["plan"]["key8"] == (form_off not in ("128", "448")), res["plan"]
+    assert res["plan"]["anchored"] == anchored, res["plan"]
+
+
+def _anchor_case(kind):
+    if kind == "edges":
+        return _frame_edge_case(141), (1 << 20) + 3
+    if kind == "late_drift":
+        return _late_drift_case(142), (1 << 20) + 3
+    if kind == "dup":
+        return make_case(seed=143, R=40, per_cs=1500, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                         n_ranks=9, tomb_frac=0.1, dup_frac=0.001, force=[(23, 700, "dup")]), (1 << 20) + 9
+    if kind == "send_overflow":
+        return make_case(seed=144, R=6, per_cs=2000, n_local=3000, n_new=800, n_ranks=7,
+                         c0=((WALL + 10) << 16) | 0xFFFE), (1 << 20) + 1
+    if kind == "hot":                                  # every key in bucket 0: split into parts
+        return make_case(seed=145, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                         n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05), (1 << 20) + 5
+    if kind == "cold":
+        case = _cold_bucket_case(146)
+        return case, case["n_ids"]
+    if kind == "one_level":                            # capacity <= 2^20: one partition level, 4-B kj
+        return make_case(seed=147, R=50, per_cs=1500, n_local=2500, n_new=1500, millis_span=6, counter_span=3,
+                         n_ranks=11, tomb_frac=0.1), None
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["edges", "late_drift", "dup", "send_overflow", "hot", "cold", "one_level"])
+def test_sorted_anchored(gpu_device, monkeypatch, kind):
+    """The anchored sorted path (the packed key's lt frame fixed from C_0 and the wall clock before
+    any record is read, the clock scan folded into the level-1 scatter, the stop point applied by the
+    resolve): rows, canonical, status and exception fields equal the oracle's, on frame edges,
+    exceptions raised in recv() (a late drift, a duplicate node) and in send(), split hot buckets,
+    cold buckets and one partition level — and the scan's path (bit 262144) gives the same."""
+    case, cap = _anchor_case(kind)
+    bound = int(case["rank"].max()) + 1
+    kw = dict(path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound, device_cols=True)
+    res = compare_with_oracle(case, **kw)
+    assert res["path"] == "sorted" and res["plan"]["anchored"] and res["plan"]["packed"], res["plan"]
+    if kind in ("late_drift", "dup", "send_overflow"):
+        assert res["status"] != 0, res
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(NO_ANCHOR))
+    res0 = compare_with_oracle(case, **kw)
+    assert not res0["plan"]["anchored"]
+
+
+@pytest.mark.parametrize("where", ["applied", "after_stop"])
+def test_sorted_anchored_frame_miss(gpu_device, where):
+    """A record older than the anchored frame reaches (2^L lt values below max(C_0, wall + 60 s) + R):
+    in an applied changeset the anchored call stores nothing and the library reruns it on the scan's
+    exact frame (plan: not anchored); in a changeset after the stop point (a late drift) it is
+    dropped with that changeset and the anchored result stands.  Both equal the oracle."""
+    case = _late_drift_case(148)                        # stop = 37 (drift at changeset 37)
+    x = int(case["offsets"][10 if where == "applied" else 41]) + 3
+    case["lt"] = case["lt"].copy()
+    case["lt"][x] = (case["wall"] - (1 << 33)) << 16     # ~100 days behind: below any anchored frame
+    bound = int(case["rank"].max()) + 1
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
+                              rank_bound=bound, device_cols=True)
+    assert res["status"] == 1 and res["n_stored"] == 37, res
+    assert res["plan"]["anchored"] == (where == "after_stop"), res["plan"]
 
 
 @pytest.mark.parametrize("L", [42, 43, 44, 45])
