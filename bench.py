@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--local", type=int, default=1 << 27)
     p.add_argument("--zipf", type=float, default=0.8)
     p.add_argument("--order", choices=["shuffled", "ascending"], default="shuffled")
+    p.add_argument("--millis-span", type=int, default=1 << 16,
+                   help="fan-in: replica clocks drawn over this many ms (2^26: replicas ~18 h apart)")
     p.add_argument("--path", choices=["auto", "gather", "sorted"], default="auto",
                    help="merge strategy (crdt_set_merge_path): gather = K2 per changeset, sorted = key-partitioned")
     p.add_argument("--no-presharded", action="store_true", help="N > 1: skip the pre-sharded figure")
@@ -132,10 +134,13 @@ def main():
     census = args.config == "fanin" and not args.no_census and world > 1      # N > 1: counted at generation
     if args.config == "fanin":
         wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                       device=dev, order=args.order, rank=rank, world=world, route=world > 1, census=census)
+                       device=dev, order=args.order, rank=rank, world=world, route=world > 1, census=census,
+                       millis_span=args.millis_span)
         workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
                     f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
                     f"{args.order} order), local map 2^{int(np.log2(args.local))} keys")
+        if args.millis_span != 1 << 16:
+            workload += f", clocks over {args.millis_span:,} ms"
         if world > 1:
             workload += (f"; replica j arrives whole on rank j % {world}, keys owned by rank key % {world}, "
                          f"records routed to their owner inside the step (one grouped all-to-all per step)")
@@ -149,10 +154,12 @@ def main():
         workload = ("cfg3: 100M-key local map, 1024 replicas x 97,657 records, Zipf(1.0) keys, millis over 8 "
                     "values x counters over 4 (ties decided by node rank)")
     else:
-        assert world == 1, "cfg5 runs on one GPU here"
-        wl = gen_cfg5(device=dev)
+        wl = gen_cfg5(device=dev, rank=rank, world=world)
         workload = ("cfg5 streaming: 100M-key table, 100 deltas x 10M records, one merge call per delta "
                     "(advancing wall), 10% tombstones, peers 1..16")
+        if world > 1:
+            workload += (f"; every delta split into {world} contiguous parts (part r on rank r), keys owned by "
+                         f"rank key % {world}: one collective merge per delta routes the records to their owners")
     torch.cuda.synchronize()
     log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
 
@@ -381,7 +388,7 @@ def main():
         roofline["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
 
     cpu = cpu16 = cpu_omp = parity = None
-    if world > 1 and args.config == "fanin" and not args.no_cpu:
+    if world > 1 and args.config in ("fanin", "cfg5") and not args.no_cpu:
         # N > 1: every rank digests its shard (one 64-bit word per 2^20 slots, after the timed path's
         # last merge); rank 0 regenerates the same batch unsharded, times the CPU baselines on it and
         # runs the OpenMP oracle over all of it, then compares every shard's digests and the
@@ -391,8 +398,11 @@ def main():
         got = [None] * world
         dist.all_gather_object(got, mine)
         if rank == 0:
-            full = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                             device=dev, order=args.order)
+            if args.config == "fanin":
+                full = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                                 device=dev, order=args.order, millis_span=args.millis_span)
+            else:
+                full = gen_cfg5(device=dev)
             cpu = cpu_baseline(full, args.cpu_seconds, args.cpu_changesets, threads=1)
             if not args.no_cpu_copy16:
                 cpu16 = cpu_baseline(full, args.cpu_seconds, args.cpu_changesets)
@@ -408,7 +418,8 @@ def main():
         del wl["home"], src, cols
         torch.cuda.empty_cache()
         pw = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                       device=dev, order=args.order, rank=rank, world=world, route=False)
+                       device=dev, order=args.order, rank=rank, world=world, route=False,
+                       millis_span=args.millis_span)
         po = pw["owned"]
         cols = (po["key"], po["lt"], po["rank"], po["val"], pw["owned_offsets"])
         table.set_presharded(True)
@@ -497,8 +508,11 @@ def pmc_kernel(args, path, name, world):
 
 def pmc_args(args) -> list:
     """The arguments that define the workload a committed PMC profile must match."""
-    return [args.config, args.records, args.replicas, args.keys, args.local, args.zipf, args.order, args.path,
-            bool(args.exact_counts)]
+    out = [args.config, args.records, args.replicas, args.keys, args.local, args.zipf, args.order, args.path,
+           bool(args.exact_counts)]
+    if args.millis_span != 1 << 16:
+        out.append(args.millis_span)
+    return out
 
 
 def cpu_baseline(wl, budget_s, n_changesets=64, threads=None):

@@ -132,7 +132,8 @@ struct Misc {
     // a bound of the rows the call wrote (k_put_*: one past the largest in-range key id;
     // k_bucket_items: the end of the last non-empty 4096-key bucket of the sorted path): the
     // table's high-water mark of written rows moves to it (crdt_ctx::hw)
-    unsigned long long key_end, key_pad;
+    unsigned long long key_end;
+    unsigned long long route_own;   // k_route_plan: 1 = the own chunk is scattered into the receive columns
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
@@ -787,16 +788,35 @@ __global__ __launch_bounds__(kScanThreads) void k_route_count(
     }
 }
 
-// kPk: the global record frame fits the sorted path's packed key, so a routed record is 16 B
-// {slot, packed (lt, rank, window changeset) in o_lt, val} instead of 20 B (o_rank unused).
-template <bool kPk>
+// Destination columns of routed records: {slot, lt (or the packed key), rank (unpacked only), val}.
+struct RouteCols {
+    uint32_t* slot;
+    int64_t* lt;
+    uint32_t* rank;
+    uint32_t* val;
+};
+
+// The wire format, decided on the device from the all-gathered frame (Misc::fr_*, k_shard_combine):
+// when the global record frame fits the sorted path's packed key (and frame_on), a routed record is
+// 16 B {slot, packed (lt, rank, window changeset) in lt, val} instead of 20 B (rank unused).  The host
+// reaches the same decision from the same words (frame_of) once it has read them back.
+__device__ inline bool route_frame(const Misc* fm, uint32_t frame_on, PackFrame* pf) {
+    *pf = make_frame(fm->fr_lo, fm->fr_hi, fm->fr_rlo, fm->fr_rhi);
+    return frame_on && pf->ok;
+}
+
+// Records for owner `me` (this rank's own chunk) go straight into the receive columns `own` at
+// their receive positions (the cursors of row me are receive positions: k_route_plan), so the apply
+// reads them in place; own.slot == nullptr: every owner's records go to `send`.
 __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
-    uint32_t jbase, uint32_t R, uint32_t G, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ o_slot,
-    int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank, uint32_t* __restrict__ o_val,
-    uint64_t* __restrict__ o_perm, PackFrame pf)
+    uint32_t jbase, uint32_t R, uint32_t G, unsigned long long* __restrict__ cursor, RouteCols send,
+    RouteCols own, uint32_t me, uint64_t* __restrict__ o_perm, const Misc* __restrict__ fm, uint32_t frame_on)
 {
+    PackFrame pf;
+    const bool pk = route_frame(fm, frame_on, &pf);
+    if (!fm->route_own) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
     const uint32_t j = jbase + blockIdx.y;
@@ -827,16 +847,17 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
             const uint64_t i = base + (uint64_t)q * kScanThreads + threadIdx.x;
             if (i < end) {
                 const uint64_t o = s_base[dst[q]] + pos[q];
-                o_slot[o] = k[q] / G;
+                const RouteCols& oc = own.slot && dst[q] == me ? own : send;
+                oc.slot[o] = k[q] / G;
                 const int64_t l = __builtin_nontemporal_load(lt + i);
                 const uint32_t r = __builtin_nontemporal_load(rank + i);
-                if (kPk) {
-                    o_lt[o] = (int64_t)pack_record(pf, l, r, j % kWindow);
+                if (pk) {
+                    oc.lt[o] = (int64_t)pack_record(pf, l, r, j % kWindow);
                 } else {
-                    o_lt[o] = l;
-                    o_rank[o] = r;
+                    oc.lt[o] = l;
+                    oc.rank[o] = r;
                 }
-                o_val[o] = __builtin_nontemporal_load(val + i);
+                oc.val[o] = __builtin_nontemporal_load(val + i);
                 if (o_perm) o_perm[o] = i;
             }
         }
@@ -914,14 +935,16 @@ __global__ __launch_bounds__(kScanThreads) void k_route_count_v(
     }
 }
 
-template <bool kPk>
 __global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
     const uint32_t* __restrict__ key, const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const uint32_t* __restrict__ val, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ tstart,
     uint32_t jbase, uint32_t R, uint32_t G, uint32_t nbits, unsigned long long* __restrict__ cursor,
-    uint32_t* __restrict__ o_slot, int64_t* __restrict__ o_lt, uint32_t* __restrict__ o_rank,
-    uint32_t* __restrict__ o_val, uint64_t* __restrict__ o_perm, PackFrame pf)
+    RouteCols send, RouteCols own, uint32_t me, uint64_t* __restrict__ o_perm, const Misc* __restrict__ fm,
+    uint32_t frame_on)
 {
+    PackFrame pf;
+    const bool pk = route_frame(fm, frame_on, &pf);
+    if (!fm->route_own) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
     const uint32_t j = jbase + blockIdx.y;
@@ -976,15 +999,17 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
                 const int q = 4 * g + x;
                 const uint64_t i = i0 + x;
                 if (i >= end) continue;
-                const uint64_t o = s_base[k[q] % G] + pos[q];
-                o_slot[o] = k[q] / G;
-                if (kPk) {
-                    o_lt[o] = (int64_t)pack_record(pf, l[x], r[x], j % kWindow);
+                const uint32_t d = k[q] % G;
+                const uint64_t o = s_base[d] + pos[q];
+                const RouteCols& oc = own.slot && d == me ? own : send;
+                oc.slot[o] = k[q] / G;
+                if (pk) {
+                    oc.lt[o] = (int64_t)pack_record(pf, l[x], r[x], j % kWindow);
                 } else {
-                    o_lt[o] = l[x];
-                    o_rank[o] = r[x];
+                    oc.lt[o] = l[x];
+                    oc.rank[o] = r[x];
                 }
-                o_val[o] = v[x];
+                oc.val[o] = v[x];
                 if (o_perm) o_perm[o] = i;
             }
         }
@@ -1001,6 +1026,62 @@ __global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt,
     const uint64_t x = (uint64_t)lt[i];
     lt[i] = (int64_t)((uint64_t)pf.lt0 + (x >> pf.sh));
     rank[i] = pf.rk0 + (uint32_t)((x >> 13) & pf.rk_mask);
+}
+
+// The route plan on the device, from the [G][R] send counts (cnt[d][j]: records of this rank's part
+// of changeset j owned by rank d) and the exchanged receive counts (rcv[s][j]: records rank s sends
+// here): cursor[d][j] = the first send position of (d, j), send columns owner-major then changeset
+// order; with own_in_recv, row `me` instead holds RECEIVE positions — rd[me] (every record received
+// from lower ranks) plus the records of this rank's own chunk in earlier changesets — so the
+// scatter writes the own chunk where the apply reads it.  One workgroup, chunks of 1024 cells.
+// own_in_recv is honoured only when every record this rank receives fits the receive columns'
+// capacity recv_cap (Misc::route_own says whether it was); the scatter reads that word.
+__global__ __launch_bounds__(1024) void k_route_plan(const unsigned long long* __restrict__ cnt,
+                                                     const unsigned long long* __restrict__ rcv, uint32_t G,
+                                                     uint32_t R, uint32_t me, uint32_t own_in_recv,
+                                                     uint64_t recv_cap, unsigned long long* __restrict__ cursor,
+                                                     Misc* __restrict__ misc)
+{
+    __shared__ unsigned long long s_wave[16];
+    __shared__ unsigned long long s_carry, s_rd;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t cells = (uint64_t)G * R;
+    auto block_scan = [&](const unsigned long long* src, uint64_t n, unsigned long long* dst) {
+        if (tid == 0) s_carry = 0;
+        __syncthreads();
+        for (uint64_t b0 = 0; b0 < n; b0 += 1024) {
+            const uint64_t i = b0 + tid;
+            const unsigned long long v = i < n ? src[i] : 0ull;
+            unsigned long long x = v;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned long long u = __shfl_up(x, off, 64);
+                if (lane >= (uint32_t)off) x += u;
+            }
+            if (lane == 63) s_wave[w] = x;
+            __syncthreads();
+            unsigned long long pre = s_carry;
+            for (uint32_t k = 0; k < w; ++k) pre += s_wave[k];
+            if (dst && i < n) dst[i] = pre + x - v;
+            __syncthreads();
+            if (tid == 0) for (int k = 0; k < 16; ++k) s_carry += s_wave[k];
+            __syncthreads();
+        }
+    };
+    block_scan(rcv, cells, nullptr);                     // nr: every record received
+    const unsigned long long nr = s_carry;
+    block_scan(rcv, (uint64_t)me * R, nullptr);          // rd[me]: records from ranks below me
+    if (tid == 0) s_rd = s_carry;
+    __syncthreads();
+    block_scan(cnt, cells, cursor);                      // send positions, owner-major
+    __threadfence_block();
+    __syncthreads();
+    const bool own = own_in_recv && nr <= recv_cap;
+    if (tid == 0) misc->route_own = own ? 1ull : 0ull;
+    if (!own) return;
+    const unsigned long long sd_me = cursor[(uint64_t)me * R];
+    __syncthreads();
+    for (uint32_t j = tid; j < R; j += 1024) cursor[(uint64_t)me * R + j] += s_rd - sd_me;
 }
 
 // Win flags of the sent records (send order, returned by the owners) -> batch order.
@@ -1324,7 +1405,9 @@ constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load 
 constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
 constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
-constexpr uint32_t kFormNoAnchor = 262144;   // the anchored sorted path off: the scan pass and the scan's frame
+constexpr uint32_t kFormAnchor = 262144;     // the anchored sorted path ON (merge_anchored; off by default:
+                                             // measured 0.25 ms slower per fan-in step)
+constexpr uint32_t kFormNoOwnInPlace = 524288; // sharded merge: the own chunk copied to the receive columns
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1416,6 +1499,7 @@ struct crdt_ctx {
     bool last_packed = false;       // the last sorted apply used the packed form
     bool anchored = false;          // this call runs the anchored sorted path (merge_anchored)
     bool last_wire_pk = false;      // the last sharded merge routed 16-B packed records
+    bool last_own_in_place = false; // ... and scattered its own chunk into the receive columns
     bool last_anchored = false;
     uint32_t anchor_skip = 0;       // calls left before the anchored frame is tried again after a miss
     bool last_key8 = false;         // ... with 1-B final key columns
@@ -1433,6 +1517,9 @@ struct crdt_ctx {
     void* rccl_comm = nullptr;
     DBuf<long long> d_gsend, d_grecv, d_pbase, d_sum;
     DBuf<unsigned long long> d_rcnt, d_rrecv;             // [G][R] route counts sent / received
+    DBuf<unsigned long long> d_rcur;                      // [G][R] scatter cursors (k_route_plan)
+    hipEvent_t route_ev = nullptr;                        // the route counts have reached the host
+    uint64_t recv_cap = 0;                                // receive columns' capacity (records)
     HBuf<uint64_t> h_rcnt;                                // both, read back once per call
     DBuf<uint32_t> r_skey, r_srank, r_sval, r_key, r_rank, r_val;   // send / receive columns
     DBuf<int64_t> r_slt, r_lt;
@@ -2501,6 +2588,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
     c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release();
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
+    c->d_rcur.release();
+    if (c->route_ev) hipEventDestroy(c->route_ev);
     if (c->table.base) hipFree(c->table.base);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
@@ -2829,7 +2918,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     c->last_anchored = false;
     PackFrame apf;
     if (frame && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
-        !(c->form_off & kFormNoAnchor) && anchored_frame(c, R, wall, &apf)) {
+        (c->form_off & kFormAnchor) && anchored_frame(c, R, wall, &apf)) {
         if (c->anchor_skip) {
             --c->anchor_skip;
         } else {
@@ -2902,6 +2991,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
+    if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;
     *flags = f;
     return CRDT_OK;
 }

@@ -198,48 +198,58 @@ def _affine(K: int, gen: torch.Generator, dev) -> tuple[int, int]:
 
 def gen_cfg5(device="cuda", K: int = 100_000_000, n_delta: int = 10_000_000, deltas: int = 100,
              tomb: float = 0.1, inject: str | None = None, inject_at: tuple[int, int] = (37, 4_999_999),
-             seed: int = 0xC0FFEE05, peers: int = 16, step_ms: int = 1000) -> dict:
+             seed: int = 0xC0FFEE05, peers: int = 16, step_ms: int = 1000, rank: int = 0,
+             world: int = 1) -> dict:
     """configs[4]: ``deltas`` merge calls of ``n_delta`` records each against a K-key table.
 
     Delta d comes from peer ``1 + d % peers`` (local node rank 0), keys = an affine bijection of
     [0, K) restricted to the first n_delta points (unique within the delta), millis in
     [base + d*step_ms, base + (d+1)*step_ms), wall_d = base + (d+1)*step_ms + 500.
     ``inject``: None, "drift" (millis = wall + 60_001) or "dup" (local rank, newest lt) at
-    ``inject_at`` = (delta, position)."""
+    ``inject_at`` = (delta, position).
+
+    ``world`` > 1 (configs[4] on N GPUs, one key-sharded replica): every delta is split into
+    ``world`` contiguous parts, part r on rank r (so the concatenation in rank order is the delta in
+    its own order: the parts protocol of include/crdt_merge.h), keys stay global ids (the library
+    routes them to their owner ``key % world``); ``home`` / ``home_offsets`` hold this rank's parts,
+    one changeset per delta, and the local table holds this rank's shard (slot = key // world)."""
     assert n_delta <= K
     dev = torch.device(device)
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed)
-    n = n_delta * deltas
+    cut = [(n_delta * r) // world for r in range(world + 1)]          # part r of a delta: [cut[r], cut[r+1])
+    mine = cut[rank + 1] - cut[rank]
+    n = mine * deltas
     key = torch.empty(n, dtype=torch.int32, device=dev)
     lt = torch.empty(n, dtype=torch.int64, device=dev)
-    rank = torch.empty(n, dtype=torch.int32, device=dev)
+    rank_c = torch.empty(n, dtype=torch.int32, device=dev)
     val = torch.empty(n, dtype=torch.int32, device=dev)
     walls = np.zeros(deltas, np.int64)
     aff = []
     i = torch.arange(n_delta, device=dev, dtype=torch.int64)
+    part = slice(cut[rank], cut[rank + 1])
     for d in range(deltas):
         a, b = _affine(K, gen, dev)
         aff.append((a, b))
-        sl = slice(d * n_delta, (d + 1) * n_delta)
-        key[sl] = ((i * a + b) % K).to(torch.int32)
+        sl = slice(d * mine, (d + 1) * mine)
+        walls[d] = BASE_MILLIS + (d + 1) * step_ms + 500
+        k_d = ((i * a + b) % K).to(torch.int32)
         ms = BASE_MILLIS + d * step_ms + torch.randint(0, step_ms, (n_delta,), device=dev, generator=gen)
-        lt[sl] = (ms << 16) + torch.randint(0, 16, (n_delta,), device=dev, generator=gen)
-        rank[sl] = 1 + d % peers
+        lt_d = (ms << 16) + torch.randint(0, 16, (n_delta,), device=dev, generator=gen)
+        r_d = torch.full((n_delta,), 1 + d % peers, dtype=torch.int32, device=dev)
         v = (d * n_delta + i + 1).to(torch.int32)
         v[torch.rand(n_delta, device=dev, generator=gen) < tomb] = -1          # NULL handle 0xFFFFFFFF
-        val[sl] = v
-        walls[d] = BASE_MILLIS + (d + 1) * step_ms + 500
-    if inject:
-        dj, pi = inject_at
-        x = dj * n_delta + pi
-        if inject == "drift":
-            lt[x] = (walls[dj] + 60_001) << 16
-        elif inject == "dup":
-            lt[x] = (walls[dj] + 1) << 16
-            rank[x] = 0
-        else:
-            raise ValueError(inject)
+        if inject and d == inject_at[0]:
+            pi = inject_at[1]
+            if inject == "drift":
+                lt_d[pi] = (walls[d] + 60_001) << 16
+            elif inject == "dup":
+                lt_d[pi] = (walls[d] + 1) << 16
+                r_d[pi] = 0
+            else:
+                raise ValueError(inject)
+        key[sl], lt[sl], rank_c[sl], val[sl] = k_d[part], lt_d[part], r_d[part], v[part]
+        del k_d, ms, lt_d, r_d, v
     lgen = torch.Generator(device=dev)
     lgen.manual_seed(seed ^ 0x5EED)
     # local rows: clocks over [base - span/2, base + 0.3 span) — the early deltas compete with them,
@@ -249,12 +259,19 @@ def gen_cfg5(device="cuda", K: int = 100_000_000, n_delta: int = 10_000_000, del
                                                    generator=lgen)
     l_lt = (l_ms << 16) + torch.randint(0, 16, (K,), device=dev, generator=lgen)
     del l_ms
-    local = {"slot": torch.arange(K, device=dev, dtype=torch.int32), "lt": l_lt,
-             "rank": torch.zeros(K, device=dev, dtype=torch.int32),
-             "val": torch.arange(K, device=dev, dtype=torch.int32), "mod": l_lt.clone()}
-    offs = (np.arange(deltas + 1, dtype=np.uint64) * n_delta)
-    return {"owned": {"key": key, "lt": lt, "rank": rank, "val": val}, "owned_offsets": offs,
-            "home": {"lt": lt, "rank": rank}, "home_offsets": offs, "local": local, "n_local_rows": K,
-            "capacity": K, "c0": int(l_lt.max().item()), "wall": int(walls[0]), "walls": walls,
-            "per_call": True, "affine": aff, "R": deltas, "n_per_replica": n_delta, "total": n, "K": K,
-            "n_local": K, "world": 1, "rank": 0}
+    c0 = int(l_lt.max().item())
+    lids = torch.arange(rank, K, world, device=dev, dtype=torch.int64)
+    local = {"slot": (lids // world).to(torch.int32), "lt": l_lt[lids].contiguous(),
+             "rank": torch.zeros(len(lids), device=dev, dtype=torch.int32),
+             "val": lids.to(torch.int32), "mod": l_lt[lids].contiguous()}
+    del l_lt
+    offs = (np.arange(deltas + 1, dtype=np.uint64) * mine)
+    cols = {"key": key, "lt": lt, "rank": rank_c, "val": val}
+    out = {"local": local, "n_local_rows": len(lids), "capacity": -(-K // world), "c0": c0, "wall": int(walls[0]),
+           "walls": walls, "per_call": True, "affine": aff, "R": deltas, "n_per_replica": n_delta,
+           "total": n_delta * deltas, "K": K, "n_local": K, "world": world, "rank": rank}
+    if world == 1:
+        out.update(owned=cols, owned_offsets=offs, home={"lt": lt, "rank": rank_c}, home_offsets=offs)
+    else:
+        out.update(owned={}, owned_offsets=None, home=cols, home_offsets=offs)
+    return out

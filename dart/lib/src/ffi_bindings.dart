@@ -87,6 +87,17 @@ typedef _MergeC = Int32 Function(
 typedef _MergeD = int Function(Pointer<Void>, Pointer<CrdtBatch>, int, Pointer<Uint8>, Pointer<CrdtResult>);
 typedef _StatusStrC = Pointer<Uint8> Function(Int32);
 typedef _StatusStrD = Pointer<Uint8> Function(int);
+// key-sharded multi-GPU (include/crdt_merge.h, "key-sharded multi-GPU")
+typedef _CommIdC = Int32 Function(Pointer<Uint8>);
+typedef _CommIdD = int Function(Pointer<Uint8>);
+typedef _CommInitC = Int32 Function(Pointer<Void>, Uint32, Uint32, Pointer<Uint8>);
+typedef _CommInitD = int Function(Pointer<Void>, int, int, Pointer<Uint8>);
+typedef _CommInfoC = Int32 Function(Pointer<Void>, Pointer<Uint32>, Pointer<Uint32>);
+typedef _CommInfoD = int Function(Pointer<Void>, Pointer<Uint32>, Pointer<Uint32>);
+typedef _CtxOnlyC = Int32 Function(Pointer<Void>);
+typedef _CtxOnlyD = int Function(Pointer<Void>);
+
+const int crdtCommIdBytes = 128;
 
 /// The library's entry points, looked up once.
 class CrdtLib {
@@ -109,7 +120,12 @@ class CrdtLib {
         setMergePath = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_merge_path'),
         setCounts = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_counts'),
         setRankBound = lib.lookupFunction<_CtxU32C, _CtxIntD>('crdt_set_rank_bound'),
-        statusString = lib.lookupFunction<_StatusStrC, _StatusStrD>('crdt_status_string');
+        statusString = lib.lookupFunction<_StatusStrC, _StatusStrD>('crdt_status_string'),
+        commUniqueId = lib.lookupFunction<_CommIdC, _CommIdD>('crdt_comm_unique_id'),
+        commInitRccl = lib.lookupFunction<_CommInitC, _CommInitD>('crdt_comm_init_rccl'),
+        commInfo = lib.lookupFunction<_CommInfoC, _CommInfoD>('crdt_comm_info'),
+        commFree = lib.lookupFunction<_CtxOnlyC, _CtxOnlyD>('crdt_comm_free'),
+        setPresharded = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_presharded');
 
   factory CrdtLib.open([String path = 'libcrdt_mi355x.so']) => CrdtLib(DynamicLibrary.open(path));
 
@@ -132,4 +148,73 @@ class CrdtLib {
   final _CtxIntD setCounts;
   final _CtxIntD setRankBound;
   final _StatusStrD statusString;
+  final _CommIdD commUniqueId;
+  final _CommInitD commInitRccl;
+  final _CommInfoD commInfo;
+  final _CtxOnlyD commFree;
+  final _CtxIntD setPresharded;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dart:ffi bindings of include/crdt_host.h (libcrdt_host.so, no GPU code): the native CrdtJson.decode
+// that GpuMapCrdt.mergeJson uses (crdt.dart:100-109, crdt_json.dart:19-37), as crdt_amd/hostlib.py does.
+const int crdtHostOk = 0;
+const int crdtHostFallback = 1; // valid input outside the fast path: decode it with CrdtJson.decode
+const int crdtHostEJson = -2; // malformed JSON: jsonDecode would throw FormatException
+
+typedef _KeysCreateC = Pointer<Void> Function();
+typedef _KeysDestroyC = Void Function(Pointer<Void>);
+typedef _KeysDestroyD = void Function(Pointer<Void>);
+typedef _KeysSizeC = Uint64 Function(Pointer<Void>);
+typedef _KeysSizeD = int Function(Pointer<Void>);
+typedef _KeysBytesC = Uint64 Function(Pointer<Void>, Uint64, Uint64);
+typedef _KeysBytesD = int Function(Pointer<Void>, int, int);
+typedef _KeysExportC = Int32 Function(Pointer<Void>, Uint64, Uint64, Pointer<Uint8>, Uint64, Pointer<Uint64>);
+typedef _KeysExportD = int Function(Pointer<Void>, int, int, Pointer<Uint8>, int, Pointer<Uint64>);
+typedef _DecodeC = Int32 Function(Pointer<Uint8>, Uint64, Pointer<Void>, Pointer<Pointer<Void>>);
+typedef _DecodeD = int Function(Pointer<Uint8>, int, Pointer<Void>, Pointer<Pointer<Void>>);
+typedef _DecNodeCountC = Uint32 Function(Pointer<Void>);
+typedef _DecColumnsC = Int32 Function(
+    Pointer<Void>, Pointer<Uint32>, Pointer<Int64>, Pointer<Uint32>, Pointer<Uint64>, Pointer<Uint32>);
+typedef _DecColumnsD = int Function(
+    Pointer<Void>, Pointer<Uint32>, Pointer<Int64>, Pointer<Uint32>, Pointer<Uint64>, Pointer<Uint32>);
+typedef _DecNodesC = Int32 Function(Pointer<Void>, Pointer<Uint8>, Uint64, Pointer<Uint64>);
+typedef _DecNodesD = int Function(Pointer<Void>, Pointer<Uint8>, int, Pointer<Uint64>);
+
+class CrdtHostLib {
+  CrdtHostLib(DynamicLibrary lib)
+      : keysCreate = lib.lookupFunction<_KeysCreateC, _KeysCreateC>('crdt_keys_create'),
+        keysDestroy = lib.lookupFunction<_KeysDestroyC, _KeysDestroyD>('crdt_keys_destroy'),
+        keysSize = lib.lookupFunction<_KeysSizeC, _KeysSizeD>('crdt_keys_size'),
+        keysBytes = lib.lookupFunction<_KeysBytesC, _KeysBytesD>('crdt_keys_bytes'),
+        keysExport = lib.lookupFunction<_KeysExportC, _KeysExportD>('crdt_keys_export'),
+        jsonDecode = lib.lookupFunction<_DecodeC, _DecodeD>('crdt_json_decode'),
+        decodedFree = lib.lookupFunction<_KeysDestroyC, _KeysDestroyD>('crdt_decoded_free'),
+        decodedCount = lib.lookupFunction<_KeysSizeC, _KeysSizeD>('crdt_decoded_count'),
+        decodedNodeCount = lib.lookupFunction<_DecNodeCountC, _KeysSizeD>('crdt_decoded_node_count'),
+        decodedColumns = lib.lookupFunction<_DecColumnsC, _DecColumnsD>('crdt_decoded_columns'),
+        decodedNodeBytes = lib.lookupFunction<_KeysSizeC, _KeysSizeD>('crdt_decoded_node_bytes'),
+        decodedNodes = lib.lookupFunction<_DecNodesC, _DecNodesD>('crdt_decoded_nodes');
+
+  /// The host library, or null when it cannot be opened (mergeJson then decodes in Dart).
+  static CrdtHostLib? tryOpen([String path = 'libcrdt_host.so']) {
+    try {
+      return CrdtHostLib(DynamicLibrary.open(path));
+    } catch (_) {
+      return null;
+    }
+  }
+
+  final _KeysCreateC keysCreate;
+  final _KeysDestroyD keysDestroy;
+  final _KeysSizeD keysSize;
+  final _KeysBytesD keysBytes;
+  final _KeysExportD keysExport;
+  final _DecodeD jsonDecode;
+  final _KeysDestroyD decodedFree;
+  final _KeysSizeD decodedCount;
+  final _KeysSizeD decodedNodeCount;
+  final _DecColumnsD decodedColumns;
+  final _KeysSizeD decodedNodeBytes;
+  final _DecNodesD decodedNodes;
 }

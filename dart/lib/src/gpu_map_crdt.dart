@@ -13,6 +13,7 @@
 // base constructor's refreshCanonicalTime() call (crdt.dart:31-33) lands in the override.
 import 'dart:async';
 import 'dart:collection';
+import 'dart:convert';
 import 'dart:ffi';
 import 'dart:typed_data';
 
@@ -105,12 +106,72 @@ class _ValueStore<V> {
 
 class GpuMapCrdt<K, V> extends Crdt<K, V> {
   GpuMapCrdt(this.nodeId,
-      [Map<K, Record<V>> seed = const {}, int device = 0, int capacity = 1024, String? library])
+      [Map<K, Record<V>> seed = const {}, int device = 0, int capacity = 1024, String? library,
+      String? hostLibrary])
       : _lib = CrdtLib.open(library ?? 'libcrdt_mi355x.so'),
         _device = device,
-        _initialCapacity = capacity {
+        _initialCapacity = capacity,
+        _hostPath = hostLibrary,
+        _nRanks = 1,
+        _shardRank = 0,
+        _commId = null {
     // (the base constructor has already run refreshCanonicalTime() on the empty map: 0)
     if (seed.isNotEmpty) _store(seed, notify: false); // map_crdt.dart:16-18: no clock refresh
+  }
+
+  /// One key shard of a replica spread over [nRanks] GPUs, one process per GPU (include/crdt_merge.h,
+  /// "key-sharded multi-GPU", in its pre-sharded form: crdt_set_presharded).  The application owns the
+  /// partition of the key space (e.g. a hash of the key modulo nRanks) and hands every process only the
+  /// records of the keys it owns — so keys, node ids and values are interned per process exactly as in
+  /// a single GpuMapCrdt, and no value handle crosses processes.  The shards join one RCCL
+  /// communicator (rank 0 draws [commId] with [commUniqueId], the application passes the 128 bytes to
+  /// every process) and their merges are COLLECTIVE: every rank calls merge / mergeAll / mergeAllBulk /
+  /// mergeJson together with its part of each changeset (changeset j = the parts in rank order, a
+  /// legal iteration order), and the library all-gathers the part maxima and reduces the first
+  /// exception, so every shard applies the same changesets and keeps the same canonical clock as the
+  /// whole replica would (crdt.dart:77-94).  getRecord / containsKey / recordMap / watch see this
+  /// shard's keys.  Local writes (put, putAll, putRecord(s), purge) would advance one shard's clock
+  /// alone, so they throw here.  No reference counterpart: the reference is one process
+  /// (example/crdt_example.dart:21-25).
+  GpuMapCrdt.sharded(this.nodeId,
+      {required int nRanks,
+      required int rank,
+      required Uint8List commId,
+      int device = 0,
+      int capacity = 1024,
+      String? library,
+      String? hostLibrary})
+      : _lib = CrdtLib.open(library ?? 'libcrdt_mi355x.so'),
+        _device = device,
+        _initialCapacity = capacity,
+        _hostPath = hostLibrary,
+        _nRanks = nRanks,
+        _shardRank = rank,
+        _commId = commId {
+    if (commId.length != crdtCommIdBytes) throw ArgumentError.value(commId.length, 'commId', 'must be 128 bytes');
+    _c; // join the communicator now: every rank constructs its shard together
+  }
+
+  /// The 128-byte RCCL unique id rank 0 draws for [GpuMapCrdt.sharded] (crdt_comm_unique_id).
+  static Uint8List commUniqueId([String? library]) {
+    final lib = CrdtLib.open(library ?? 'libcrdt_mi355x.so');
+    final p = calloc<Uint8>(crdtCommIdBytes);
+    try {
+      final st = lib.commUniqueId(p);
+      if (st != crdtOk) throw StateError('crdt_comm_unique_id: ${lib.statusString(st).cast<Utf8>().toDartString()}');
+      return Uint8List.fromList(p.asTypedList(crdtCommIdBytes));
+    } finally {
+      calloc.free(p);
+    }
+  }
+
+  final int _nRanks;
+  final int _shardRank;
+  final Uint8List? _commId;
+  bool get _sharded => _commId != null;
+
+  void _localOnly(String what) {
+    if (_sharded) throw UnsupportedError('$what on a key shard: local writes belong to a single-replica GpuMapCrdt');
   }
 
   @override
@@ -119,6 +180,17 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   final CrdtLib _lib;
   final int _device;
   final int _initialCapacity;
+  final String? _hostPath;
+  CrdtHostLib? _hostLib;
+  bool _hostTried = false;
+
+  CrdtHostLib? get _host {
+    if (!_hostTried) {
+      _hostTried = true;
+      _hostLib = CrdtHostLib.tryOpen(_hostPath ?? 'libcrdt_host.so');
+    }
+    return _hostLib;
+  }
   Pointer<Void> _ctx = nullptr;
   final _keyIds = <K, int>{};
   final _keys = <K>[];
@@ -137,6 +209,16 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
         _check(_lib.create(_device, _nodes.rank(nodeId), _initialCapacity, out), 'crdt_create');
         _ctx = out.value;
         _check(_lib.setRankBound(_ctx, _nodes.sorted.length), 'crdt_set_rank_bound');
+        if (_commId != null) {
+          final id = calloc<Uint8>(crdtCommIdBytes);
+          try {
+            id.asTypedList(crdtCommIdBytes).setAll(0, _commId!);
+            _check(_lib.commInitRccl(_ctx, _nRanks, _shardRank, id), 'crdt_comm_init_rccl');
+            _check(_lib.setPresharded(_ctx, 1), 'crdt_set_presharded'); // key ids are this shard's slots
+          } finally {
+            calloc.free(id);
+          }
+        }
       } finally {
         calloc.free(out);
       }
@@ -145,6 +227,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   }
 
   void close() {
+    if (_ctx != nullptr && _sharded) _lib.commFree(_ctx);
     if (_ctx != nullptr) _lib.destroy(_ctx);
     _ctx = nullptr;
     _controller.close();
@@ -305,10 +388,16 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   }
 
   @override
-  void putRecord(K key, Record<V> value) => _store({key: value}, notify: true); // map_crdt.dart:27-30
+  void putRecord(K key, Record<V> value) {
+    _localOnly('putRecord');
+    _store({key: value}, notify: true); // map_crdt.dart:27-30
+  }
 
   @override
-  void putRecords(Map<K, Record<V>> recordMap) => _store(recordMap, notify: true); // map_crdt.dart:33-39
+  void putRecords(Map<K, Record<V>> recordMap) {
+    _localOnly('putRecords');
+    _store(recordMap, notify: true); // map_crdt.dart:33-39
+  }
 
   @override
   Map<K, Record<V>> recordMap({Hlc? modifiedSince}) {
@@ -349,6 +438,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   @override
   void purge() {
     // map_crdt.dart:52
+    _localOnly('purge');
     _check(_lib.clearRows(_c, 0, _keys.length), 'crdt_clear_rows');
     _keyIds.clear();
     _keys.clear();
@@ -389,6 +479,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
   void putAll(Map<K, V?> values) {
     // crdt.dart:46-54: ONE Hlc.send for the call, every record {C, value, C}
     if (values.isEmpty) return;
+    _localOnly('putAll');
     final n0 = _keys.length;
     final n = values.length;
     final kid = calloc<Uint32>(n), val = calloc<Uint32>(n);
@@ -429,9 +520,74 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
 
   @override
   void mergeJson(String json, {KeyDecoder<K>? keyDecoder, ValueDecoder<V>? valueDecoder}) {
-    // crdt.dart:100-109.  (libcrdt_host.so's crdt_json_decode can replace CrdtJson.decode for
-    // the wire format CrdtJson.encode writes: INTEGRATION.md, "The host library from Dart".)
-    merge(CrdtJson.decode<K, V>(json, canonicalTime, keyDecoder: keyDecoder, valueDecoder: valueDecoder));
+    // crdt.dart:100-109.  Without decoders the document is decoded by libcrdt_host.so's
+    // crdt_json_decode (JSON parse, Hlc.parse and key interning in C++, as MapCrdt.mergeJson of
+    // crdt_amd/crdt.py does); input outside its fast path, or no host library, falls back to
+    // CrdtJson.decode, so the map merged is the same either way.
+    final native = keyDecoder == null && valueDecoder == null ? _decodeNative(json) : null;
+    merge(native ??
+        CrdtJson.decode<K, V>(json, canonicalTime, keyDecoder: keyDecoder, valueDecoder: valueDecoder));
+  }
+
+  /// CrdtJson.decode (crdt_json.dart:19-37) through crdt_json_decode: the document's keys in their
+  /// order (a repeated key keeps its first position and its last record, as jsonDecode does), each
+  /// Hlc from its logical time and node id (Hlc.parse, hlc.dart:39-46), each value jsonDecode-d from
+  /// its span.  The `modified` placeholder (crdt_json.dart:23-24) never survives merge.  Null: fall back.
+  Map<K, Record<V>>? _decodeNative(String json) {
+    final host = _host;
+    if (host == null || '' is! K) return null; // keys are the document's strings (`key as K`)
+    final bytes = utf8.encode(json);
+    final src = calloc<Uint8>(bytes.isEmpty ? 1 : bytes.length);
+    final keys = host.keysCreate();
+    final out = calloc<Pointer<Void>>();
+    try {
+      src.asTypedList(bytes.length).setAll(0, bytes);
+      final st = host.jsonDecode(src, bytes.length, keys, out);
+      if (st == crdtHostFallback) return null;
+      if (st == crdtHostEJson) throw FormatException('crdt_json_decode: malformed JSON');
+      if (st != crdtHostOk) throw StateError('crdt_json_decode: $st');
+      final d = out.value;
+      try {
+        final n = host.decodedCount(d);
+        final nk = host.keysSize(keys);
+        final kb = host.keysBytes(keys, 0, nk);
+        final kbuf = calloc<Uint8>(kb == 0 ? 1 : kb), koff = calloc<Uint64>(nk + 1);
+        final nn = host.decodedNodeCount(d), nb = host.decodedNodeBytes(d);
+        final nbuf = calloc<Uint8>(nb == 0 ? 1 : nb), noff = calloc<Uint64>(nn + 1);
+        final m = n == 0 ? 1 : n;
+        final kid = calloc<Uint32>(m), node = calloc<Uint32>(m), vlen = calloc<Uint32>(m);
+        final lt = calloc<Int64>(m), voff = calloc<Uint64>(m);
+        try {
+          if (host.keysExport(keys, 0, nk, kbuf, kb, koff) != crdtHostOk ||
+              host.decodedNodes(d, nbuf, nb, noff) != crdtHostOk ||
+              host.decodedColumns(d, kid, lt, node, voff, vlen) != crdtHostOk) {
+            return null;
+          }
+          final kt = kbuf.asTypedList(kb == 0 ? 1 : kb), nt = nbuf.asTypedList(nb == 0 ? 1 : nb);
+          final keyStr = [for (var i = 0; i < nk; ++i) utf8.decode(kt.sublist(koff[i], koff[i + 1]))];
+          final nodes = <dynamic>[for (var i = 0; i < nn; ++i) utf8.decode(nt.sublist(noff[i], noff[i + 1]))];
+          final modified = canonicalTime;
+          final result = <K, Record<V>>{};
+          for (var i = 0; i < n; ++i) {
+            final dynamic value =
+                vlen[i] == 0 ? null : jsonDecode(utf8.decode(bytes.sublist(voff[i], voff[i] + vlen[i])));
+            result[keyStr[kid[i]] as K] =
+                Record<V>(Hlc<dynamic>.fromLogicalTime(lt[i], nodes[node[i]]), value as V?, modified);
+          }
+          return result;
+        } finally {
+          for (final p in <Pointer>[kbuf, koff, nbuf, noff, kid, node, vlen, lt, voff]) {
+            calloc.free(p);
+          }
+        }
+      } finally {
+        host.decodedFree(d);
+      }
+    } finally {
+      host.keysDestroy(keys);
+      calloc.free(src);
+      calloc.free(out);
+    }
   }
 
   /// `for (m in changesets) merge(m)` as ONE device call: R sequential merges batched

@@ -276,11 +276,14 @@ enum crdt_plan_flags {
     CRDT_PLAN_KEY16 = 32,        /* ... and 14-B level-1 records (2-B key column) */
     CRDT_PLAN_HIGH_WATER = 64,   /* ... and its resolve did not read the rows at or above the table's
                                     high-water mark of written rows (never-written fill) */
-    CRDT_PLAN_ANCHORED = 128,    /* ... on the anchored frame: the packed key's lt range fixed before any
-                                    record is read (every applied record is <= max(C_0, wall + 60 s) + R,
-                                    hlc.dart:92-94), the clock scan folded into the level-1 scatter */
-    CRDT_PLAN_WIRE_PACKED = 256  /* sharded ctx: records crossed the all-to-all as 16-B packed
+    CRDT_PLAN_ANCHORED = 128,    /* ... on the anchored frame (opt-in, CRDT_SORTED_FORM bit 262144): the
+                                    packed key's lt range fixed before any record is read (every applied
+                                    record is <= max(C_0, wall + 60 s) + R, hlc.dart:92-94), the clock
+                                    scan folded into the level-1 scatter */
+    CRDT_PLAN_WIRE_PACKED = 256, /* sharded ctx: records crossed the all-to-all as 16-B packed
                                     {slot, (lt, rank, changeset) key, val} instead of 20 B */
+    CRDT_PLAN_OWN_IN_PLACE = 512 /* sharded ctx: the records this rank owns of its own batch were
+                                    scattered straight into the receive columns (no device copy) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

@@ -9,11 +9,15 @@
  *      (CRDT_MEM_HOST) — the library's collective path with its exchanges done by this file,
  *   4. the sorted path again on 32-B rows (crdt_set_row_bytes) with the batch's rank bound declared
  *      (crdt_set_rank_bound: max rank + 1),
+ *   5. a 1-rank pre-sharded ctx (crdt_set_presharded) over the loopback table — what
+ *      GpuMapCrdt.sharded (dart/lib/src/gpu_map_crdt.dart) sets up,
+ *   6. the same over a 1-rank RCCL communicator (crdt_comm_unique_id + crdt_comm_init_rccl),
  * and compares status, stop point, exception fields, canonical, win flags and every row with
- * the expected values, bit for bit.  Exit status 0 = all equal.
+ * the expected values, bit for bit.  It also decodes a CrdtJson document with libcrdt_host.so's
+ * crdt_json_decode (what GpuMapCrdt.mergeJson calls) and checks its columns.  Exit status 0 = all equal.
  *
  *   gcc -O2 -std=c11 -I include tests/c/abi_golden.c -o tests/c/abi_golden \
- *       -L crdt_amd -l:libcrdt_mi355x.so -Wl,-rpath,'$ORIGIN/../../crdt_amd'
+ *       -L crdt_amd -l:libcrdt_mi355x.so -l:libcrdt_host.so -Wl,-rpath,'$ORIGIN/../../crdt_amd'
  *   tests/c/abi_golden tests/golden/abi_cases.bin
  */
 #include <stdint.h>
@@ -21,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "crdt_host.h"
 #include "crdt_merge.h"
 
 typedef struct {
@@ -145,7 +150,8 @@ static int check(const Case* c, crdt_ctx* ctx, int rc, const crdt_result* res, c
 }
 
 /* mode 0: gather + flags; 1: sorted, no flags; 2: 1-rank sharded ctx over the loopback table;
- * 3: sorted on 32-B rows with a declared rank bound */
+ * 3: sorted on 32-B rows with a declared rank bound; 4: 1-rank pre-sharded ctx, loopback table;
+ * 5: 1-rank pre-sharded ctx over RCCL */
 static int run(const Case* c, int mode) {
     crdt_ctx* ctx = NULL;
     int st = crdt_create(0, c->local_rank, c->n_ids, &ctx);
@@ -176,13 +182,25 @@ static int run(const Case* c, int mode) {
     b.key_id = c->key; b.lt = c->lt; b.rank = c->rank; b.val = c->val; b.millis = c->millis;
     b.offsets = c->offsets; b.n_changesets = c->R; b.mem = CRDT_MEM_HOST;
     uint8_t* flags = NULL;
-    const char* what = mode == 0 ? "gather" : mode == 1 ? "sorted" : mode == 2 ? "sharded-1" : "sorted-32B-bound";
+    const char* what = mode == 0 ? "gather" : mode == 1 ? "sorted" : mode == 2 ? "sharded-1" : mode == 3 ? "sorted-32B-bound"
+                     : mode == 4 ? "presharded-1" : "presharded-1-rccl";
     if (mode == 0) {
         crdt_set_merge_path(ctx, CRDT_PATH_GATHER);
         flags = calloc(c->n ? c->n : 1, 1);
     } else if (mode == 1 || mode == 3) {
         crdt_set_merge_path(ctx, CRDT_PATH_SORTED);
         crdt_set_counts(ctx, 0);
+    } else if (mode == 5) {
+        uint8_t id[CRDT_COMM_ID_BYTES];
+        uint32_t nr = 0, rk = 9;
+        if ((st = crdt_comm_unique_id(id)) != CRDT_OK || (st = crdt_comm_init_rccl(ctx, 1, 0, id)) != CRDT_OK ||
+            (st = crdt_set_presharded(ctx, 1)) != CRDT_OK || (st = crdt_comm_info(ctx, &nr, &rk)) != CRDT_OK ||
+            nr != 1 || rk != 0) {
+            fprintf(stderr, "mode 5 setup: %s\n", crdt_status_string(st));
+            crdt_destroy(ctx);
+            return 1;
+        }
+        flags = calloc(c->n ? c->n : 1, 1);
     } else {
         crdt_comm_ops ops;
         memset(&ops, 0, sizeof(ops));
@@ -191,6 +209,7 @@ static int run(const Case* c, int mode) {
         ops.all_gather_i64 = lb_all_gather;
         ops.all_to_all_v = lb_all_to_all;
         st = crdt_comm_init_ops(ctx, 1, 0, &ops);
+        if (st == CRDT_OK && mode == 4) st = crdt_set_presharded(ctx, 1);
         if (st != CRDT_OK) { fprintf(stderr, "crdt_comm_init_ops: %s\n", crdt_status_string(st)); crdt_destroy(ctx); return 1; }
         flags = calloc(c->n ? c->n : 1, 1);
     }
@@ -205,9 +224,52 @@ static int run(const Case* c, int mode) {
         counted = path != CRDT_PATH_SORTED;
     }
     int bad = check(c, ctx, rc, &res, flags, what, counted);
-    if (mode == 2 && c->R && lb_calls == calls0) { fprintf(stderr, "[%s/%s] the communicator was never called\n", c->name, what); bad = 1; }
+    if ((mode == 2 || mode == 4) && c->R && lb_calls == calls0) { fprintf(stderr, "[%s/%s] the communicator was never called\n", c->name, what); bad = 1; }
+    if (mode == 5) crdt_comm_free(ctx);
     free(flags);
     crdt_destroy(ctx);
+    return bad;
+}
+
+/* CrdtJson.decode of a small document through libcrdt_host.so (crdt_json.dart:19-37, hlc.dart:39-46):
+ * keys in document order, lt = (millis << 16) + counter, node ids in first-seen order, value spans
+ * (length 0 = null). */
+static int json_decode_check(void) {
+    static const char doc[] =
+        "{\"k0\":{\"hlc\":\"2024-01-01T00:00:00.000Z-0000-node_b\",\"value\":1},"
+        "\"k1\":{\"hlc\":\"2024-01-01T00:00:00.001Z-000A-node_c\",\"value\":null},"
+        "\"k2\":{\"hlc\":\"2024-01-01T00:00:01.000Z-FFFF-node_b\",\"value\":\"x\"}}";
+    crdt_keys* keys = crdt_keys_create();
+    crdt_decoded* d = NULL;
+    int bad = 0;
+    int st = crdt_json_decode(doc, sizeof(doc) - 1, keys, &d);
+    if (st != CRDT_HOST_OK || !d || crdt_decoded_count(d) != 3 || crdt_decoded_node_count(d) != 2) {
+        fprintf(stderr, "crdt_json_decode: status %d\n", st);
+        bad = 1;
+    } else {
+        uint32_t kid[3], node[3], vlen[3];
+        int64_t lt[3];
+        uint64_t voff[3], noff[3];
+        char nodes[64];
+        crdt_decoded_columns(d, kid, lt, node, voff, vlen);
+        crdt_decoded_nodes(d, nodes, sizeof(nodes), noff);
+        const int64_t ms = 1704067200000ll;
+        const int64_t want_lt[3] = {ms << 16, ((ms + 1) << 16) + 0xA, ((ms + 1000) << 16) + 0xFFFF};
+        const uint32_t want_node[3] = {0, 1, 0}, want_len[3] = {1, 0, 3};
+        for (int i = 0; i < 3; ++i)
+            if (kid[i] != (uint32_t)i || lt[i] != want_lt[i] || node[i] != want_node[i] || vlen[i] != want_len[i]) {
+                fprintf(stderr, "crdt_json_decode record %d: key %u lt %lld node %u len %u\n", i, kid[i],
+                        (long long)lt[i], node[i], vlen[i]);
+                bad = 1;
+            }
+        if (memcmp(nodes + noff[0], "node_b", 6) != 0 || memcmp(nodes + noff[1], "node_c", 6) != 0 ||
+            memcmp(doc + voff[2], "\"x\"", 3) != 0) {
+            fprintf(stderr, "crdt_json_decode: node ids / value spans differ\n");
+            bad = 1;
+        }
+    }
+    if (d) crdt_decoded_free(d);
+    crdt_keys_destroy(keys);
     return bad;
 }
 
@@ -235,10 +297,12 @@ int main(int argc, char** argv) {
     for (uint32_t k = 0; k < nc; ++k) {
         Case c;
         read_case(&c);
-        for (int mode = 0; mode < 4; ++mode, ++runs) bad |= run(&c, mode);
+        for (int mode = 0; mode < 6; ++mode, ++runs) bad |= run(&c, mode);
     }
-    printf("abi_golden: %u cases x 4 modes (gather + flags, sorted, 1-rank sharded over a C loopback "
-           "communicator, sorted on 32-B rows with a rank bound): %s\n", nc, bad ? "MISMATCH" : "all equal");
+    bad |= json_decode_check();
+    printf("abi_golden: %u cases x 6 modes (gather + flags, sorted, 1-rank sharded over a C loopback "
+           "communicator, sorted on 32-B rows with a rank bound, 1-rank pre-sharded over the loopback and "
+           "over RCCL) + crdt_json_decode: %s\n", nc, bad ? "MISMATCH" : "all equal");
     (void)runs;
     return bad ? 1 : 0;
 }

@@ -211,3 +211,97 @@ def test_cfg5_full_scale_injection(gpu_device, inject):
     assert np.array_equal(grank, row_rank.cpu().numpy().astype(np.uint32))
     assert np.array_equal(gval, (row_val.cpu().numpy() & 0xFFFFFFFF).astype(np.uint32))
     assert np.array_equal(gmod, row_mod.cpu().numpy())
+
+
+def _cfg5_shard_worker(rank, world, port, q, kw):
+    """One rank of configs[4] on N GPUs at reduced size: its parts of every delta, one collective
+    routed crdt_merge per delta (gloo communicator, all ranks on cuda:0)."""
+    import os
+
+    import torch.distributed as dist
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.dist import GlooComm
+    from crdt_amd.workload import gen_cfg5
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wl = gen_cfg5(device="cuda", rank=rank, world=world, **kw)
+        t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+        t.set_row_bytes(32)
+        loc, home, offs = wl["local"], wl["home"], wl["home_offsets"]
+        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        t.canonical = wl["c0"]
+        t.comm_init_ops(world, rank, GlooComm(dist))
+        results, mid = [], None
+        for d in range(wl["R"]):
+            b, e = int(offs[d]), int(offs[d + 1])
+            res, _ = t.merge(home["key"][b:e], home["lt"][b:e], home["rank"][b:e], home["val"][b:e],
+                             np.array([0, e - b], np.uint64), int(wl["walls"][d]), win_flags=False)
+            results.append(res)
+            if d == 9:
+                mid = t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))
+            if res["status"] != 0:
+                break
+        q.put((rank, results, mid, t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))))
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("inject", [None, "drift"])
+def test_cfg5_two_rank_streaming_vs_oracle(gpu_device, inject):
+    """configs[4] ('8 x MI355X streaming') rehearsed with 2 ranks on one GPU over gloo at reduced size
+    (400K keys, 40 deltas x 100K records, 10 % tombstones): every delta split into 2 contiguous parts,
+    one collective routed merge per delta, a drift injected at (37, 49,999) (on rank 0's part: the
+    exception index is the position in the whole delta).  Every call's status, stop point, exception
+    fields and canonical on both ranks, and both shards' rows after delta 9 and at the end, against
+    the C oracle merging the whole deltas in order (crdt.dart:77-94)."""
+    import torch.multiprocessing as mp
+
+    from crdt_amd.workload import gen_cfg5
+    from oracle.oracle_c import OracleTable
+    from tests.test_dist_cpu import _free_port
+    kw = dict(K=400_000, n_delta=100_000, deltas=40, inject=inject, inject_at=(37, 49_999))
+    wl = gen_cfg5(device="cuda", **kw)
+    own = {k: _np(v, np.int64) for k, v in wl["owned"].items()}
+    loc = wl["local"]
+    o = OracleTable(wl["capacity"], 0, wl["c0"])
+    o.put_rows(_np(loc["slot"], np.uint32), _np(loc["lt"], np.int64), _np(loc["rank"], np.uint32),
+               _np(loc["val"], np.uint32), _np(loc["mod"], np.int64))
+    offs = wl["owned_offsets"]
+    expect, mid_rows = [], None
+    for d in range(wl["R"]):
+        b, e = int(offs[d]), int(offs[d + 1])
+        r, _ = o.merge(own["key"][b:e].astype(np.uint32), own["lt"][b:e], own["rank"][b:e].astype(np.uint32),
+                       own["val"][b:e].astype(np.uint32), np.array([0, e - b], np.uint64), int(wl["walls"][d]),
+                       want_flags=False)
+        expect.append(r.as_dict())
+        if d == 9:
+            mid_rows = o.rows.copy()
+        if r.status != 0:
+            break
+    del wl
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg5_shard_worker, args=(r, world, port, q, kw)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, results, mid, final in outs:
+        assert len(results) == len(expect), (rank, len(results), len(expect))
+        for d, (got, want) in enumerate(zip(results, expect)):
+            for f in FIELDS:
+                assert got[f] == want[f], (rank, d, f, got[f], want[f])
+        for rows, ref in ((mid, mid_rows), (final, o.rows)):
+            sh = ref[rank::world]
+            for f, a in zip(("lt", "rank", "val", "mod"), rows):
+                assert np.array_equal(a[:len(sh)], sh[f]), (rank, f)
+    assert (expect[-1]["status"] != 0) == (inject is not None)
+    if inject:
+        assert (expect[-1]["exc_changeset"], expect[-1]["exc_index"]) == (37, 49_999)

@@ -267,7 +267,8 @@ def _make_injected(kw):
     return case
 
 
-def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path="gather", counts=True):
+def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path="gather", counts=True,
+                      again=False):
     """One rank of a sharded replica on cuda:0: the library's collective crdt_merge
     (comm_path.inc) over RCCL (backend nccl) or the host-staged gloo communicator."""
     import os
@@ -289,10 +290,14 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         loc = case["local"]
         ids = np.arange(case["n_local"])
         mine = (ids % world == rank) & (loc["mod"] != ABSENT_MOD)
-        if mine.any():
-            t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
-                       loc["val"][mine], loc["mod"][mine])
-        t.canonical = case["c0"]
+
+        def reset():
+            t.clear_rows(0, cap)
+            if mine.any():
+                t.put_rows((ids[mine] // world).astype(np.uint32), loc["lt"][mine], loc["rank"][mine],
+                           loc["val"][mine], loc["mod"][mine])
+            t.canonical = case["c0"]
+        reset()
         if backend == "nccl":
             attach_rccl(t, dist)
         else:
@@ -306,8 +311,11 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
             np.ascontiguousarray(a.view(np.int32) if a.dtype == np.uint32 else a)).cuda()
         millis = None if case["millis"] is None else dev(case["millis"][sel])
         flags = torch.zeros(max(len(sel), 1), dtype=torch.uint8, device="cuda") if path == "gather" else False
-        res, _ = t.merge(dev(key.astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]),
-                         dev(case["val"][sel]), part_offs, case["wall"], millis=millis, win_flags=flags)
+        cols = (dev(key.astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]), dev(case["val"][sel]))
+        res, _ = t.merge(*cols, part_offs, case["wall"], millis=millis, win_flags=flags)
+        if again:                 # the same call again on this ctx (receive columns sized by the first)
+            reset()
+            res, _ = t.merge(*cols, part_offs, case["wall"], millis=millis, win_flags=flags)
         res["path"] = t.last_path()
         res["plan"] = t.last_plan()
         lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
@@ -318,7 +326,7 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         dist.destroy_process_group()
 
 
-def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True):
+def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True, again=False):
     import torch.multiprocessing as mp
 
     from tests.test_dist_cpu import _free_port, layout
@@ -327,7 +335,7 @@ def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_gpu_worker, args=(r, world, port, kw, kind, q, backend, path, counts))
+    procs = [ctx.Process(target=_shard_gpu_worker, args=(r, world, port, kw, kind, q, backend, path, counts, again))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -370,6 +378,18 @@ def test_two_rank_routed_sorted_path(gpu_device, counts):
               n_ranks=301)
     outs = run_shard_gpu(kw, 3, "parts", path="sorted", counts=counts)
     assert all(o[1]["path"] == "sorted" for o in outs)
+
+
+@pytest.mark.parametrize("kind", ["routed", "parts"])
+@pytest.mark.parametrize("path", ["gather", "sorted"])
+@pytest.mark.parametrize("name", ["r8_tombstones", "drift_late", "explicit_millis"])
+def test_two_rank_own_chunk_in_place(gpu_device, name, kind, path):
+    """The second collective merge on each ctx scatters the rank's own chunk straight into the
+    receive columns (sized by the first call; CRDT_PLAN_OWN_IN_PLACE): every shard row, canonical and
+    exception fields vs the oracle, gather and sorted receivers (win flags keep the copy)."""
+    outs = run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path=path, counts=path == "gather", again=True)
+    for rank, res, *_ in outs:
+        assert res["plan"]["own_in_place"] == (path != "gather"), (rank, res["plan"])
 
 
 @pytest.mark.parametrize("kind", ["routed", "parts"])
@@ -483,9 +503,10 @@ def test_eight_rank_routed_packed_sorted(gpu_device, inject):
     8 shards, the canonical clock, status and exception fields against the C oracle."""
     kw = dict(seed=808, R=64, per_cs=250_000, n_local=1_500_000, n_new=600_000, millis_span=1 << 12,
               counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
-    outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False)
+    outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False, again=True)
     for rank, res, *_ in outs:
         assert res["path"] == "sorted" and res["plan"]["wire_packed"], (rank, res["plan"])
+        assert res["plan"]["own_in_place"], (rank, res["plan"])        # the second call on each ctx
         assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
         if inject:
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
@@ -676,7 +697,6 @@ def test_sorted_hist_in_scan(gpu_device, monkeypatch, kind, cap):
     """The level-1 histogram counted by the scan (device columns, rank bound, order-free form):
     same rows / result as the oracle and as the separate histogram pass (CRDT_HIST_FUSE=0),
     including a stop < R (rows of the unapplied changesets' tiles cleared) and one / two levels."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(NO_ANCHOR))     # the scan's path, not the anchored one
     if kind == "edges":
         case = _frame_edge_case(95)
     elif kind == "late_drift":
@@ -739,7 +759,7 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
     t.close()
 
 
-NO_ANCHOR = 262144        # CRDT_SORTED_FORM bit: the anchored sorted path off (the scan pass runs)
+ANCHOR = 262144           # CRDT_SORTED_FORM bit: the anchored sorted path on (default: the scan pass)
 
 
 @pytest.mark.parametrize("anchored", [True, False])
@@ -749,7 +769,7 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off, anchored
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
     level-2 histogram with 2-B loads into shared bins, the level-1 scatter's / the scan's narrow
     loads, 32K-record level-2 tiles) gives the same rows, on the anchored path and the scan's."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (0 if anchored else NO_ANCHOR)))
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (ANCHOR if anchored else 0)))
     case = _frame_edge_case(99)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
@@ -775,7 +795,7 @@ def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_
     """Every CRDT_SORTED_FORM switch on records spread over many cold buckets, two levels: the
     unsplit-bucket resolve of each form (the changed-rows-only writes with 13-B final records
     among them) against the oracle, anchored and not."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (0 if anchored else NO_ANCHOR)))
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (ANCHOR if anchored else 0)))
     case = _cold_bucket_case(131)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=case["n_ids"],
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
@@ -813,7 +833,8 @@ def test_sorted_anchored(gpu_device, monkeypatch, kind):
     any record is read, the clock scan folded into the level-1 scatter, the stop point applied by the
     resolve): rows, canonical, status and exception fields equal the oracle's, on frame edges,
     exceptions raised in recv() (a late drift, a duplicate node) and in send(), split hot buckets,
-    cold buckets and one partition level — and the scan's path (bit 262144) gives the same."""
+    cold buckets and one partition level — and the scan's path (the default) gives the same."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(ANCHOR))
     case, cap = _anchor_case(kind)
     bound = int(case["rank"].max()) + 1
     kw = dict(path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound, device_cols=True)
@@ -821,17 +842,18 @@ def test_sorted_anchored(gpu_device, monkeypatch, kind):
     assert res["path"] == "sorted" and res["plan"]["anchored"] and res["plan"]["packed"], res["plan"]
     if kind in ("late_drift", "dup", "send_overflow"):
         assert res["status"] != 0, res
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(NO_ANCHOR))
+    monkeypatch.setenv("CRDT_SORTED_FORM", "0")
     res0 = compare_with_oracle(case, **kw)
     assert not res0["plan"]["anchored"]
 
 
 @pytest.mark.parametrize("where", ["applied", "after_stop"])
-def test_sorted_anchored_frame_miss(gpu_device, where):
+def test_sorted_anchored_frame_miss(gpu_device, monkeypatch, where):
     """A record older than the anchored frame reaches (2^L lt values below max(C_0, wall + 60 s) + R):
     in an applied changeset the anchored call stores nothing and the library reruns it on the scan's
     exact frame (plan: not anchored); in a changeset after the stop point (a late drift) it is
     dropped with that changeset and the anchored result stands.  Both equal the oracle."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", str(ANCHOR))
     case = _late_drift_case(148)                        # stop = 37 (drift at changeset 37)
     x = int(case["offsets"][10 if where == "applied" else 41]) + 3
     case["lt"] = case["lt"].copy()

@@ -25,6 +25,12 @@ for stage in ${STAGE:-tests}; do
       timeout -k 10 ${TLIM:-600} python -u bench.py --no-cpu --no-census --no-pcie --steps ${ABSTEPS:-8} --warmup 2 \
         --ab "$AB" ${BENCH_ARGS:-} > gpurun_out/r03_ab_${TAG}.json 2> gpurun_out/r03_ab_${TAG}.log
       rc=$?; grep "A/B" gpurun_out/r03_ab_${TAG}.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/r03_ab_${TAG}.log; exit $rc; } ;;
+    route8)   # config 4's N = 8 path rehearsed with 8 ranks on one GPU over the gloo crdt_comm_ops table
+      CRDT_BENCH_BACKEND=gloo timeout -k 10 ${TLIM:-600} python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node ${NR:-8} --master-addr 127.0.0.1 --master-port ${PORT:-29517} bench.py --gpus ${NR:-8} \
+        --records ${RECS:-16000000} --steps 2 --warmup 1 --cpu-seconds 3 ${BENCH_ARGS:-} \
+        > gpurun_out/r03_bench_route${NR:-8}_gloo.json 2> gpurun_out/r03_bench_route${NR:-8}_gloo.log
+      rc=$?; cat gpurun_out/r03_bench_route${NR:-8}_gloo.json; [ $rc -eq 0 ] || { tail -30 gpurun_out/r03_bench_route${NR:-8}_gloo.log; exit $rc; } ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

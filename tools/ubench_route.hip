@@ -52,8 +52,15 @@ int main() {
     CK(hipMalloc(&d_offs, (R + 1) * 8)); CK(hipMalloc(&d_tstart, (R + 1) * 4));
     CK(hipMemcpy(d_offs, offs.data(), (R + 1) * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_tstart, ts.data(), (R + 1) * 4, hipMemcpyHostToDevice));
-    PackFrame pf = make_frame(~ord64((int64_t)(1735689600000ull << 16)), ord64((int64_t)(((1735689600000ull + 65536) << 16) | 15)), 0, 0);
-    pf.rk0 = 0; pf.rk_span = 1025; pf.sh = 11 + 13; pf.rk_mask = (1u << 11) - 1;
+    // the frame words the library's scatter reads (Misc::fr_*: lt over the fill's range, ranks 0..1025)
+    Misc hm{};
+    hm.fr_lo = ~ord64((int64_t)(1735689600000ull << 16));
+    hm.fr_hi = ord64((int64_t)(((1735689600000ull + 65536) << 16) | 15));
+    hm.fr_rlo = ~0u;
+    hm.fr_rhi = 1025;
+    Misc* fm;
+    CK(hipMalloc(&fm, sizeof(Misc)));
+    CK(hipMemcpy(fm, &hm, sizeof(Misc), hipMemcpyHostToDevice));
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     for (uint32_t G : {8u, 2u}) {
@@ -82,10 +89,11 @@ int main() {
                     for (uint32_t j = 0; j < R; ++j) { hcur[(size_t)d * R + j] = so; so += hc[v][(size_t)d * R + j]; }
                 CK(hipMemcpy(cur, hcur.data(), cells * 8, hipMemcpyHostToDevice));
                 CK(hipEventRecord(a));
-                if (v == 0) k_route_scatter<true><<<grid, kScanThreads>>>(key, lt, rank, val, d_offs, d_tstart, 0, R, G, cur,
-                                                                       o_slot, o_lt, o_rank, o_val, o_perm, pf);
-                else k_route_scatter_v<true><<<grid, kScanThreads>>>(key, lt, rank, val, d_offs, d_tstart, 0, R, G, nbits, cur,
-                                                                     o_slot, o_lt, o_rank, o_val, o_perm, pf);
+                const RouteCols snd{o_slot, o_lt, o_rank, o_val}, none{nullptr, nullptr, nullptr, nullptr};
+                if (v == 0) k_route_scatter<<<grid, kScanThreads>>>(key, lt, rank, val, d_offs, d_tstart, 0, R, G, cur,
+                                                                    snd, none, 0, o_perm, fm, 1u);
+                else k_route_scatter_v<<<grid, kScanThreads>>>(key, lt, rank, val, d_offs, d_tstart, 0, R, G, nbits, cur,
+                                                               snd, none, 0, o_perm, fm, 1u);
                 CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
                 CK(hipEventElapsedTime(&ms, a, b)); best_s = std::min(best_s, ms);
             }
