@@ -800,8 +800,8 @@ struct RouteCols {
 // when the global record frame fits the sorted path's packed key (and frame_on), a routed record is
 // 16 B {slot, packed (lt, rank, window changeset) in lt, val} instead of 20 B (rank unused).  The host
 // reaches the same decision from the same words (frame_of) once it has read them back.
-__device__ inline bool route_frame(const Misc* fm, uint32_t frame_on, PackFrame* pf) {
-    *pf = make_frame(fm->fr_lo, fm->fr_hi, fm->fr_rlo, fm->fr_rhi);
+__device__ inline bool route_frame(const Misc* fm, uint32_t frame_on, uint32_t R, PackFrame* pf) {
+    *pf = make_frame(fm->fr_lo, fm->fr_hi, fm->fr_rlo, fm->fr_rhi, R);
     return frame_on && pf->ok;
 }
 
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
     RouteCols own, uint32_t me, uint64_t* __restrict__ o_perm, const Misc* __restrict__ fm, uint32_t frame_on)
 {
     PackFrame pf;
-    const bool pk = route_frame(fm, frame_on, &pf);
+    const bool pk = route_frame(fm, frame_on, R, &pf);
     if (!fm->route_own) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
                 const int64_t l = __builtin_nontemporal_load(lt + i);
                 const uint32_t r = __builtin_nontemporal_load(rank + i);
                 if (pk) {
-                    oc.lt[o] = (int64_t)pack_record(pf, l, r, j % kWindow);
+                    oc.lt[o] = (int64_t)pack_record(pf, l, r, j % pf.jwin);
                 } else {
                     oc.lt[o] = l;
                     oc.rank[o] = r;
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
     uint32_t frame_on)
 {
     PackFrame pf;
-    const bool pk = route_frame(fm, frame_on, &pf);
+    const bool pk = route_frame(fm, frame_on, R, &pf);
     if (!fm->route_own) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
                 const RouteCols& oc = own.slot && d == me ? own : send;
                 oc.slot[o] = k[q] / G;
                 if (pk) {
-                    oc.lt[o] = (int64_t)pack_record(pf, l[x], r[x], j % kWindow);
+                    oc.lt[o] = (int64_t)pack_record(pf, l[x], r[x], j % pf.jwin);
                 } else {
                     oc.lt[o] = l[x];
                     oc.rank[o] = r[x];
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt,
     if (i >= n) return;
     const uint64_t x = (uint64_t)lt[i];
     lt[i] = (int64_t)((uint64_t)pf.lt0 + (x >> pf.sh));
-    rank[i] = pf.rk0 + (uint32_t)((x >> 13) & pf.rk_mask);
+    rank[i] = pack_rank(pf, x);
 }
 
 // The route plan on the device, from the [G][R] send counts (cnt[d][j]: records of this rank's part
@@ -1349,6 +1349,13 @@ __global__ __launch_bounds__(256) void k_remap(Table table, uint64_t n,
 }
 
 // ============================================================ host-side context
+// CRDT_POISON_ALLOC=1 (debug): every scratch allocation is filled with 0x5A bytes, so a kernel that
+// reads scratch it never wrote gives the same wrong answer on every run instead of stale data's
+static bool poison_alloc() {
+    static const int v = [] { const char* e = getenv("CRDT_POISON_ALLOC"); return e && atoi(e) ? 1 : 0; }();
+    return v != 0;
+}
+
 template <typename T>
 struct DBuf {
     T* p = nullptr;
@@ -1359,6 +1366,10 @@ struct DBuf {
         size_t m = std::max<size_t>(want, 16);
         hipError_t e = hipMalloc(&p, m * sizeof(T));
         if (e == hipSuccess) n = m;
+        if (e == hipSuccess && poison_alloc()) {      // (finished before any stream's next use)
+            e = hipMemset(p, 0x5A, m * sizeof(T));
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+        }
         return e;
     }
     void release() { if (p) hipFree(p); p = nullptr; n = 0; }
@@ -1853,7 +1864,7 @@ PackFrame frame_of(const crdt_ctx* c) {
     const bool bound = c->frame_lt_only;
     const uint32_t rlo = bound ? (any ? ~0u : 0u) : m->fr_rlo;               // ~min: min 0
     const uint32_t rhi = bound ? (any ? c->rank_bound - 1 : 0u) : m->fr_rhi;
-    PackFrame f = make_frame(m->fr_lo, m->fr_hi, rlo, rhi);
+    PackFrame f = make_frame(m->fr_lo, m->fr_hi, rlo, rhi, c->plan_R);
     f.rk_limit = bound ? c->rank_bound : UINT32_MAX;
     return f;
 }
@@ -2074,10 +2085,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     c->last_key16 = k16;
     c->last_hw = pk && !c->counts && c->hw_read < c->cap;     // (in the first window)
     for (size_t sb = 0; sb < ns_all;) {
-        const uint32_t jb = sg.j[sb] - sg.j[sb] % kWindow;          // window [jb, jb + kWindow)
+        // window [jb, jb + win): kWindow changesets (the kj word's field), the packed key's W
+        const uint32_t win = pk ? pf.jwin : kWindow;
+        const uint32_t jb = sg.j[sb] - sg.j[sb] % win;
         size_t se = sb;
         uint64_t nw = 0;
-        while (se < ns_all && sg.j[se] < jb + kWindow) { nw += sg.end[se] - sg.beg[se]; ++se; }
+        while (se < ns_all && sg.j[se] < jb + win) { nw += sg.end[se] - sg.beg[se]; ++se; }
         const uint32_t nseg = (uint32_t)(se - sb);
         const size_t s0 = sb;
         sb = se;
@@ -2412,21 +2425,23 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
 // the anchor off for the next calls of this ctx.
 bool anchored_frame(const crdt_ctx* c, uint32_t R, int64_t wall, PackFrame* out) {
     if (!c->rank_bound) return false;
-    const uint64_t r1 = c->rank_bound;                   // rank fields 0 .. bound - 1, bound = clamp
-    int K = 0;
-    while (K < 64 && (r1 >> K) != 0) ++K;
-    const int L = 60 - (K + 13);
+    const int K = bitlen64(c->rank_bound);               // rank fields 0 .. bound - 1, bound = clamp
+    uint32_t jb = 0, jwin = 0;
+    if (!frame_window(60 - K - 13, K, R, &jb, &jwin) || jwin < R) return false;   // one window
+    const int L = 60 - (K + (int)jb);
     if (L < 30) return false;                            // under ~16 s of millis: not worth a miss
     const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
     const int64_t b = imax(c->canonical, wp);
     if (b > INT64_MAX - (int64_t)R - 1) return false;
     const int64_t top = b + (int64_t)R;
     PackFrame f;
-    f.lt_span = (1ull << L) - 2;                         // span + 1 has L bits (make_frame's rule)
+    f.lt_span = (1ull << L) - 1;                         // the lt field: L bits (make_frame's rule)
     f.lt0 = (int64_t)((uint64_t)top - f.lt_span);
     f.rk0 = 0;
     f.rk_span = c->rank_bound - 1;
-    f.sh = (uint32_t)(K + 13);
+    f.jb = jb;
+    f.jwin = jwin;
+    f.sh = (uint32_t)K + jb;
     f.rk_mask = (1ull << K) - 1;
     f.rk_limit = c->rank_bound;
     f.ok = true;

@@ -43,6 +43,15 @@ def check_device_tensor(t, kind: str, device: int, name: str = "tensor"):
         raise ValueError(f"{name} is on cuda:{t.device.index}, the table on cuda:{device}")
 
 
+def torch_ready(t):
+    """The library reads device columns on its own HIP stream, but torch produced them on torch's
+    current stream (asynchronously): that stream's pending work on the tensor's device is finished
+    before the pointer is handed over (the C-ABI's contract: resident columns are ready when a crdt_*
+    call starts; the call itself returns only when its stream is done, so outputs need nothing)."""
+    import torch
+    torch.cuda.current_stream(t.device).synchronize()
+
+
 class _Cols:
     """Normalises a set of columns to one memory kind and keeps them alive."""
 
@@ -59,6 +68,8 @@ class _Cols:
                     arr = arr.numpy()
                 else:
                     check_device_tensor(arr, kind, device, f"column {name}")
+                    if not self.keep or not _is_torch(self.keep[0]):
+                        torch_ready(arr)
                     mem = _capi.CRDT_MEM_DEVICE
                     self._set_mem(mem)
                     self.keep.append(arr)
@@ -105,6 +116,7 @@ class DeviceTable:
     def _dptr(self, t, kind: str, name: str):
         """Device pointer of a GPU tensor argument after the width / device checks."""
         check_device_tensor(t, kind, self.device, name)
+        torch_ready(t)
         return ctypes.c_void_p(t.data_ptr())
 
     def _check(self, st: int, what: str):
@@ -214,6 +226,7 @@ class DeviceTable:
             if c.mem == _capi.CRDT_MEM_DEVICE:
                 import torch
                 flags_arr = torch.zeros(max(n, 1), dtype=torch.uint8, device=c.keep[0].device)
+                torch_ready(flags_arr)                  # (its zero fill must not land after the merge)
                 fptr = ctypes.c_void_p(flags_arr.data_ptr())
             else:
                 flags_arr = np.zeros(max(n, 1), np.uint8)

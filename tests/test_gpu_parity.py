@@ -865,26 +865,47 @@ def test_sorted_anchored_frame_miss(gpu_device, monkeypatch, where):
     assert res["plan"]["anchored"] == (where == "after_stop"), res["plan"]
 
 
-@pytest.mark.parametrize("L", [42, 43, 44, 45])
+@pytest.mark.parametrize("L", [44, 45, 46, 47])
 def test_sorted_key8_frame_boundary(gpu_device, L):
-    """The 1-B key column needs 4 free bits above the packed key (L + K + 13 <= 60, L / K the lt /
-    rank field widths): lt spans on both sides of that boundary, stretched downwards by old
-    records (no clock effect) — key8 on / off as the frame says, same rows as the oracle."""
-    case = make_case(seed=98 + L, R=40, per_cs=1500, n_local=2500, n_new=1500, millis_span=4,
+    """The 1-B key column needs 4 free bits above the packed key (L + K + J <= 60; L / K / J the lt /
+    rank / changeset field widths, J = bitlen(min(R, 4096) + 1)): lt spans on both sides of that
+    boundary, stretched downwards by old records (no clock effect) — key8 on / off as the frame
+    says, same rows as the oracle."""
+    R = 2000
+    case = make_case(seed=98 + L, R=R, per_cs=60, n_local=2500, n_new=1500, millis_span=4,
                      counter_span=3, n_ranks=9, tomb_frac=0.1)
     rng = np.random.default_rng(L)
     lt = case["lt"].copy()
     hi = int(lt.max())
     pick = np.nonzero(rng.random(len(lt)) < 0.02)[0]
     lt[pick] = hi - rng.integers(0, 1 << (L - 1), len(pick))
-    lt[pick[0]] = hi - ((1 << (L - 1)) + 5)                     # lt span + 1 has exactly L bits
+    lt[pick[0]] = hi - ((1 << (L - 1)) + 5)                     # lt span has exactly L bits
     case["lt"] = lt
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 17)
     assert res["path"] == "sorted" and res["plan"]["packed"], res["plan"]
     span = int(lt.max()) - int(lt.min())
-    assert (span + 1).bit_length() == L
+    assert span.bit_length() == L
     K = (int(case["rank"].max()) - int(case["rank"].min()) + 1).bit_length()
-    assert res["plan"]["key8"] == (L + K + 13 <= 60), (L, K, res["plan"])
+    J = (min(R, 4096) + 1).bit_length()
+    assert res["plan"]["key8"] == (L + K + J <= 60), (L, K, J, res["plan"])
+
+
+@pytest.mark.parametrize("R", [1500, 3000])
+def test_sorted_wide_frame_narrow_window(gpu_device, R):
+    """A frame too wide for the full 13-bit changeset field (L + K + 13 > 64, L + K <= 54): the
+    packed key narrows its window to the changesets that fit (>= 1022 per window, several windows
+    per call) and stays packed — same rows as the oracle."""
+    case = make_case(seed=77 + R, R=R, per_cs=50, n_local=3000, n_new=1000, millis_span=4,
+                     counter_span=3, n_ranks=9, tomb_frac=0.1)
+    rng = np.random.default_rng(R)
+    lt = case["lt"].copy()
+    hi = int(lt.max())
+    pick = np.nonzero(rng.random(len(lt)) < 0.02)[0]
+    lt[pick] = hi - rng.integers(0, 1 << 48, len(pick))
+    lt[pick[0]] = hi - ((1 << 49) + 3)                          # L = 50
+    case["lt"] = lt
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 19)
+    assert res["path"] == "sorted" and res["plan"]["packed"], res["plan"]
 
 
 def test_sorted_wide_frame_takes_list_form(gpu_device):
@@ -896,7 +917,7 @@ def test_sorted_wide_frame_takes_list_form(gpu_device):
     old = rng.random(len(case["lt"])) < 0.05
     case["lt"] = np.where(old, rng.integers(1, 1 << 20, len(case["lt"])), case["lt"]).astype(np.int64)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 9)
-    assert res["path"] == "sorted"
+    assert res["path"] == "sorted" and not res["plan"]["packed"], res["plan"]
 
 
 @pytest.mark.parametrize("packed", ["1", "0"])
