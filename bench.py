@@ -67,6 +67,8 @@ def parse():
                    help="skip cpu_baseline_copy16 (the faithful port with its map copy on 16 threads)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-census", action="store_true", help="skip the distinct-key census (B_alg job)")
+    p.add_argument("--flag-steps", type=int, default=2,
+                   help="steps of the same merge with per-record win flags, timed after the census (N = 1)")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) sample")
     p.add_argument("--exact-counts", action="store_true",
                    help="per-record n_present / n_won also on the sorted path (its changeset-ordered form)")
@@ -285,6 +287,7 @@ def main():
 
     # ---- whole-job algorithmic bytes: distinct keys touched / won
     job = {}
+    with_flags = None
     if not args.no_census and wl.get("per_call"):
         # streaming: every call is its own merge, so U is counted per call (= its records)
         reset()
@@ -311,6 +314,24 @@ def main():
         job["records_won_total"] = int(r2["n_won"])
         job["census"] = ("U_touch = distinct batch keys present in the local map, U_win = distinct keys of the "
                          "records stored (win flags of one untimed merge)")
+        # the same merge with per-record win flags (what Crdt.merge's removeWhere / watch need,
+        # crdt.dart:80-90): timed like the headline steps, beside it
+        if args.flag_steps > 0:
+            fl_ms = []
+            for _ in range(args.flag_steps):
+                reset()
+                barrier()
+                ts = time.perf_counter()
+                r3 = step(flags=flags)
+                barrier()
+                fl_ms.append((time.perf_counter() - ts) * 1e3)
+            assert r3["status"] == 0 and r3["canonical_lt"] == res["canonical_lt"], (r3, res)
+            fm = float(np.mean(fl_ms))
+            with_flags = {"ms_per_step": round(fm, 3), "value": round(total_records / (fm / 1e3), 1),
+                          "unit": "records/s", "merge_path": table.last_path(),
+                          "step_ms_all": [round(x, 3) for x in fl_ms],
+                          "what": "same job with a 1-B win flag per record (crdt_merge win_flags): the gather "
+                                  "path, which decides each record in changeset order (DESIGN 5.4)"}
     elif census:
         u_touch = all_sum(wl["u_touch"])
         # U_win: rows the merge stamped — mod >= c0 after the timed merge, less the local rows
@@ -464,7 +485,7 @@ def main():
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
         "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
-        "pcie_inclusive": pcie, "presharded": presharded,
+        "pcie_inclusive": pcie, "presharded": presharded, "with_win_flags": with_flags,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),
                          "route": round(tsum.get("route_ms", 0) / K, 3),

@@ -234,6 +234,54 @@ static int run(const Case* c, int mode) {
 /* CrdtJson.decode of a small document through libcrdt_host.so (crdt_json.dart:19-37, hlc.dart:39-46):
  * keys in document order, lt = (millis << 16) + counter, node ids in first-seen order, value spans
  * (length 0 = null). */
+/* mergeJson's second half (crdt.dart:100-109 -> merge, crdt.dart:77-94) as the Dart / Python shims
+ * run it: the decoded columns (node ids remapped to ranks in String.compareTo order beside the local
+ * node "node_a": node_b -> 1, node_c -> 2; value handles = record index, null = 0xFFFFFFFF) merged
+ * as one changeset into an empty map on the device.  Every record wins (no local row), every stored
+ * row carries modified = R_1 = max(C_0, max lt) and the canonical ends at send(R_1). */
+static int json_merge_check(const uint32_t* kid, const int64_t* lt, const uint32_t* node, const uint32_t* vlen,
+                            const int64_t* want_lt) {
+    crdt_ctx* ctx = NULL;
+    int st = crdt_create(0, 0, 16, &ctx);
+    if (st != CRDT_OK) { fprintf(stderr, "json merge: crdt_create: %s\n", crdt_status_string(st)); return 1; }
+    uint32_t rank[3], val[3];
+    for (int i = 0; i < 3; ++i) {
+        rank[i] = node[i] + 1;
+        val[i] = vlen[i] == 0 ? 0xFFFFFFFFu : (uint32_t)i;
+    }
+    const uint64_t offs[2] = {0, 3};
+    crdt_batch b;
+    memset(&b, 0, sizeof(b));
+    b.key_id = kid; b.lt = lt; b.rank = rank; b.val = val; b.millis = NULL;
+    b.offsets = offs; b.n_changesets = 1; b.mem = CRDT_MEM_HOST;
+    const int64_t wall = (want_lt[2] >> 16) + 5000;               /* 5 s after the newest record */
+    crdt_result res;
+    memset(&res, 0, sizeof(res));
+    uint8_t flags[3] = {0, 0, 0};
+    int bad = 0;
+    st = crdt_merge(ctx, &b, wall, flags, &res);
+    const int64_t r1 = want_lt[2];                               /* C_0 = 0 < every lt */
+    const int64_t c1 = (r1 + 1) > (wall << 16) ? r1 + 1 : wall << 16;
+    if (st != CRDT_OK || res.status != 0 || res.canonical_lt != c1 || !flags[0] || !flags[1] || !flags[2]) {
+        fprintf(stderr, "json merge: st %d status %d canonical %lld (want %lld)\n", st, (int)res.status,
+                (long long)res.canonical_lt, (long long)c1);
+        bad = 1;
+    } else {
+        int64_t glt[3], gmod[3];
+        uint32_t grank[3], gval[3];
+        st = crdt_read_rows(ctx, kid, 3, glt, grank, gval, gmod, CRDT_MEM_HOST);
+        for (int i = 0; i < 3 && st == CRDT_OK; ++i)
+            if (glt[i] != want_lt[i] || grank[i] != rank[i] || gval[i] != val[i] || gmod[i] != r1) {
+                fprintf(stderr, "json merge row %d: lt %lld rank %u val %u mod %lld\n", i, (long long)glt[i],
+                        grank[i], gval[i], (long long)gmod[i]);
+                bad = 1;
+            }
+        if (st != CRDT_OK) { fprintf(stderr, "json merge: crdt_read_rows: %s\n", crdt_status_string(st)); bad = 1; }
+    }
+    crdt_destroy(ctx);
+    return bad;
+}
+
 static int json_decode_check(void) {
     static const char doc[] =
         "{\"k0\":{\"hlc\":\"2024-01-01T00:00:00.000Z-0000-node_b\",\"value\":1},"
@@ -267,6 +315,7 @@ static int json_decode_check(void) {
             fprintf(stderr, "crdt_json_decode: node ids / value spans differ\n");
             bad = 1;
         }
+        if (!bad) bad = json_merge_check(kid, lt, node, vlen, want_lt);
     }
     if (d) crdt_decoded_free(d);
     crdt_keys_destroy(keys);
