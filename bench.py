@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 TIMING_EVERY = 8           # streaming configs (one merge call per delta): HIP-event timing sampled
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_bench.json")    # rocprofv3 --pmc of the default command
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_bench.json")    # rocprofv3 --pmc of the default command
 
 
 def log(*a):
@@ -310,7 +310,7 @@ def main():
         present = torch.zeros(wl["capacity"], dtype=torch.bool, device=dev)
         present[loc["slot"].long()] = loc["mod"] >= 0
         u_touch, u_win = int((seen & present).sum().item()), int(won.sum().item())
-        del flags, seen, won, present
+        del seen, won, present
         job["records_won_total"] = int(r2["n_won"])
         job["census"] = ("U_touch = distinct batch keys present in the local map, U_win = distinct keys of the "
                          "records stored (win flags of one untimed merge)")
@@ -332,6 +332,7 @@ def main():
                           "step_ms_all": [round(x, 3) for x in fl_ms],
                           "what": "same job with a 1-B win flag per record (crdt_merge win_flags): the gather "
                                   "path, which decides each record in changeset order (DESIGN 5.4)"}
+        del flags
     elif census:
         u_touch = all_sum(wl["u_touch"])
         # U_win: rows the merge stamped — mod >= c0 after the timed merge, less the local rows

@@ -308,4 +308,5 @@ def test_cfg5_two_rank_streaming_vs_oracle(gpu_device, inject):
                 assert np.array_equal(a[:len(sh)], sh[f]), (rank, f)
     assert (expect[-1]["status"] != 0) == (inject is not None)
     if inject:
-        assert (expect[-1]["exc_changeset"], expect[-1]["exc_index"]) == (37, 49_999)
+        # one call per delta: the drift stops call 37 at its record 49,999 (changeset 0 of that call)
+        assert (len(expect), expect[-1]["exc_changeset"], expect[-1]["exc_index"]) == (38, 0, 49_999)

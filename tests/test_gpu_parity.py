@@ -857,7 +857,7 @@ def test_sorted_anchored_frame_miss(gpu_device, monkeypatch, where):
     case = _late_drift_case(148)                        # stop = 37 (drift at changeset 37)
     x = int(case["offsets"][10 if where == "applied" else 41]) + 3
     case["lt"] = case["lt"].copy()
-    case["lt"][x] = (case["wall"] - (1 << 33)) << 16     # ~100 days behind: below any anchored frame
+    case["lt"][x] = (case["wall"] - (1 << 37)) << 16     # ~4 years behind: below any anchored frame
     bound = int(case["rank"].max()) + 1
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=bound, device_cols=True)

@@ -14,4 +14,4 @@ rc=$?; echo "[write] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_write.
 CMD=$(python3 -c "
 import json, sys; sys.argv=['bench.py']+'$ARGS'.split(); sys.path.insert(0,'.')
 import bench; a=bench.parse(); print(json.dumps({'command_args': bench.pmc_args(a), 'merge_path': 'sorted', 'command': 'python bench.py $ARGS'}))")
-python3 tools/pmc_step.py gpurun_out/pmc_fetch gpurun_out/pmc_write 3 gpurun_out/r02_pmc_bench.json "$CMD"
+python3 tools/pmc_step.py gpurun_out/pmc_fetch gpurun_out/pmc_write 3 gpurun_out/${PMC_OUT:-r03_pmc_bench.json} "$CMD"
