@@ -1046,7 +1046,9 @@ __global__ __launch_bounds__(1024) void k_route_plan(const unsigned long long* _
     __shared__ unsigned long long s_carry, s_rd;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t cells = (uint64_t)G * R;
+    // (starts with a barrier: every thread has read the previous scan's s_carry before it is reset)
     auto block_scan = [&](const unsigned long long* src, uint64_t n, unsigned long long* dst) {
+        __syncthreads();
         if (tid == 0) s_carry = 0;
         __syncthreads();
         for (uint64_t b0 = 0; b0 < n; b0 += 1024) {
