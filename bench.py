@@ -327,11 +327,28 @@ def main():
                 fl_ms.append((time.perf_counter() - ts) * 1e3)
             assert r3["status"] == 0 and r3["canonical_lt"] == res["canonical_lt"], (r3, res)
             fm = float(np.mean(fl_ms))
+            fpath, fplan = table.last_path(), table.last_plan()
             with_flags = {"ms_per_step": round(fm, 3), "value": round(total_records / (fm / 1e3), 1),
-                          "unit": "records/s", "merge_path": table.last_path(),
+                          "unit": "records/s", "merge_path": fpath, "flagged_form": bool(fplan.get("flagged")),
                           "step_ms_all": [round(x, 3) for x in fl_ms],
-                          "what": "same job with a 1-B win flag per record (crdt_merge win_flags): the gather "
-                                  "path, which decides each record in changeset order (DESIGN 5.4)"}
+                          "what": "same job with a 1-B win flag per record (crdt_merge win_flags, what Crdt.merge's "
+                                  "removeWhere and watch() need): the sorted path's flagged form (stable level 2, "
+                                  "ordered resolve, flags carried back to input order; DESIGN 5.4)"}
+            if fpath == "sorted" and not args.no_cpu:
+                # the same merge on the gather path (K2 decides each record in changeset order): its
+                # flags, counts and canonical must equal the flagged form's, record for record
+                reset()
+                g_flags = torch.zeros_like(flags)
+                table.set_merge_path("gather")
+                ts = time.perf_counter()
+                r4 = step(flags=g_flags)
+                torch.cuda.synchronize()
+                g_ms = (time.perf_counter() - ts) * 1e3
+                table.set_merge_path(args.path)
+                with_flags["gather_ms"] = round(g_ms, 3)
+                with_flags["flags_equal_gather"] = bool(torch.equal(g_flags, flags))
+                with_flags["counts_equal_gather"] = (r4["n_won"], r4["n_present"]) == (r3["n_won"], r3["n_present"])
+                del g_flags
         del flags
     elif census:
         u_touch = all_sum(wl["u_touch"])

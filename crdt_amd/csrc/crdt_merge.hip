@@ -1518,6 +1518,15 @@ struct crdt_ctx {
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
     bool last_hw = false;           // ... whose packed resolve skipped the rows >= hw_read
+    // per-record win flags on the sorted path (the flagged form, sorted_path.inc): CRDT_FLAGS_SORTED=0
+    // keeps every flagged merge on the gather path
+    bool flags_sorted = true;
+    bool last_flagged = false;      // the last sorted apply was the flagged form
+    DBuf<uint32_t> f_pos1, f_pos2;  // level-1 position per input record, level-2 position per level-1 one
+    DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
+    DBuf<unsigned long long> f_cin_key;   // split buckets: every part's carry-in
+    DBuf<uint32_t> f_cin_val;
+    DBuf<uint8_t> f_cin_pres;
     bool keys_checked = false;      // the gather apply checked every key id before storing
     bool resolved = false;          // misc->stop / result already computed for this plan
     crdt_timing last_timing{};
@@ -1876,7 +1885,8 @@ PackFrame frame_of(const crdt_ctx* c) {
 // over the ranks first, so every rank returns the same result.
 int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64_t n, bool sorted,
                  crdt_result* out) {
-    const bool counted = !sorted || c->counts;          // the order-free sorted form does not count them
+    // the order-free sorted form does not count them (the flagged form does)
+    const bool counted = !sorted || c->counts || c->last_flagged;
     if (c->has_comm) {
         HIPALLOC(c->d_sum.ensure(4));
         HIPALLOC(c->h_sum.ensure(4));
@@ -2050,8 +2060,11 @@ void prof_resolve_report() {
 // (tile maxima from the level-1 scatter, recurrence, exception scan, stop point) run between the
 // level-1 scatter and level 2 instead of before this function.
 int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
-                 crdt_result* out, const PackFrame* anchor = nullptr) {
+                 crdt_result* out, const PackFrame* anchor = nullptr, uint8_t* dflags = nullptr) {
     const uint32_t R = c->plan_R;
+    // dflags (device, zeroed by the caller): the flagged form — packed records, stable level 2, the
+    // ordered resolve with per-record flags, and the flags carried back to input order
+    const bool fl = dflags != nullptr;
     if (!c->resolved && !anchor)
         k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
     c->resolved = false;
@@ -2069,13 +2082,14 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     if (anchor) {
         pf = *anchor;
         pk = true;
-    } else if (cols.packed_in || (!c->counts && c->packed_resolve && c->frame_on)) {
+    } else if (cols.packed_in || ((!c->counts || fl) && c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         pf = frame_of(c);
         pk = pf.ok;
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
+    if (fl && (!pk || anchor || cols.packed_in)) return CRDT_E_INVALID;      // apply_segs checked the frame
     c->last_packed = pk;
     c->key_end_valid = true;                 // k_bucket_items bounds the rows every window writes
     c->last_hist1_fused = false;
@@ -2085,7 +2099,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
     c->last_key16 = k16;
-    c->last_hw = pk && !c->counts && c->hw_read < c->cap;     // (in the first window)
+    c->last_hw = pk && (!c->counts || fl) && c->hw_read < c->cap;     // (in the first window)
+    if (fl) {
+        uint64_t ncol = 0;                                           // input index space of pos1
+        for (size_t s = 0; s < ns_all; ++s) ncol = std::max<uint64_t>(ncol, sg.end[s]);
+        HIPALLOC(c->f_pos1.ensure(ncol ? ncol : 1));
+    }
     for (size_t sb = 0; sb < ns_all;) {
         // window [jb, jb + win): kWindow changesets (the kj word's field), the packed key's W
         const uint32_t win = pk ? pf.jwin : kWindow;
@@ -2174,7 +2193,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
         const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
         const AnchorArgs an{c->d_T.p, c->d_candtile.p, wsub(imax(c->canonical, wp), pf.lt0), c->local_rank};
-        if (anchor && k16)
+        if (fl && k16)          // the flagged form: each record's level-1 position kept at its input index
+            k_part_scatter1<true, false, true, kL1Items, true, true, false, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p);
+        else if (fl)
+            k_part_scatter1<true, false, false, kL1Items, true, false, false, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p);
+        else if (anchor && k16)
             k_part_scatter1<true, false, true, kL1AnchorItems, true, true, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
@@ -2260,7 +2289,18 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             // bound would leave the upper XCDs' ranges past the last tile, idle)
             const uint32_t nt2s = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const uint32_t xper2 = c->xcd_map ? (nt2s + kXcds - 1) / kXcds : 0;
-            if (c->counts)
+            if (fl) {          // stable: each final bucket in changeset order; level-2 positions kept
+                HIPALLOC(c->f_pos2.ensure(nw));
+                if (k16)
+                    k_part_scatter2<true, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                else if (k8)
+                    k_part_scatter2<true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                else
+                    k_part_scatter2<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+            } else if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
             else if (pk)
@@ -2299,7 +2339,47 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
-        if (c->counts) {
+        if (fl) {          // the ordered packed resolve with flags (sorted_path.inc, "win flags")
+            uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
+            uint32_t* ps_val = c->p_ksu32.p;
+            const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
+            HIPALLOC(c->f_cin_key.ensure(ksn));
+            HIPALLOC(c->f_cin_val.ensure(ksn));
+            HIPALLOC(c->f_cin_pres.ensure(ksn));
+            HIPALLOC(c->f_flag2.ensure(nw));
+            if (k8)
+                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
+                    ps_val, pf, c->d_misc);
+            else
+                k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
+                    ps_val, pf, c->d_misc);
+            k_part_cin_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+                d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
+                reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
+            const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
+            if (k8)
+                k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
+                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, c->f_flag2.p);
+            else
+                k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
+                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, c->f_flag2.p);
+            // flags back: level-2 order -> level-1 order (two levels) -> input order
+            const uint8_t* f1 = c->f_flag2.p;
+            if (two) {
+                HIPALLOC(c->f_flag1.ensure(nw));
+                k_flags_back2<<<std::min<uint32_t>(grid_for(nw, 1024), 8192), 256, 0, c->stream>>>(
+                    c->f_pos2.p, c->f_flag2.p, c->p_l1beg.p + kDigits, c->d_misc, c->f_flag1.p);
+                f1 = c->f_flag1.p;
+                // level 2 reused the tile -> segment index: rebuild level 1's
+                k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
+                                                                                                 c->p_tseg.p);
+            }
+            k_flags_back1<<<nt1, 1024, 0, c->stream>>>(tm1, c->d_misc, c->f_pos1.p, f1, dflags);
+        } else if (c->counts) {
             k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                     c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
             k_part_carry<false><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(d_hot, d_ib, d_hb, c->table,
@@ -2371,7 +2451,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
 // header) and either CRDT_MERGE_PATH=sorted or the batch is a multi-changeset fan-in
 // large enough to amortise the partition passes.  R = changesets of the call.
 bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* win_flags) {
-    if (c->merge_path == 1 || win_flags || c->canonical < 0 || c->cap > kSortedMaxCap) return false;
+    if (c->merge_path == 1 || c->canonical < 0 || c->cap > kSortedMaxCap) return false;
+    // per-record win flags: the flagged form (packed records, one ctx; apply_segs checks the frame)
+    if (win_flags && (!c->flags_sorted || c->has_comm || !c->packed_resolve)) return false;
     uint64_t n = 0, nw = 0;
     uint32_t jb = 0;
     for (size_t s = 0; s < sg.j.size(); ++s) {              // < 2^31 records per kWindow changesets
@@ -2384,8 +2466,8 @@ bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* wi
     // auto: a many-changeset fan-in.  Order-free (no per-record counts): the partitioned passes
     // beat R K2 launches from 64 changesets and 8M records on (1B fan-in: 31.4 vs 34.1 ms,
     // DESIGN.md §5); with exact counts only while changesets are small (cfg3), where K2's
-    // launches are latency-bound
-    return R >= 64 && n >= (8ull << 20) && (!c->counts || n / R <= (256ull << 10));
+    // launches are latency-bound; the flagged form counts exactly (its resolve walks in order)
+    return R >= 64 && n >= (8ull << 20) && (win_flags || !c->counts || n / R <= (256ull << 10));
 }
 
 // Apply phase over columns whose changeset segments are c->segs (n = column length).
@@ -2393,10 +2475,25 @@ int apply_segs(crdt_ctx* c, const Cols& cols, uint64_t n, int32_t mem, int64_t w
                uint8_t* win_flags, crdt_result* out, bool allow_sorted) {
     if (c->timing) HIPCHK(ensure_events(c, events_for(c->segs.j.size())));
     c->last_sorted = allow_sorted && use_sorted(c, c->segs, c->plan_R, win_flags);
+    c->last_flagged = false;
+    if (c->last_sorted && win_flags) {
+        // the flagged form runs on the packed key: the scan's frame must fit it (else K2)
+        bool ok = mem == CRDT_MEM_DEVICE && c->frame_on && !cols.packed_in;
+        if (ok) {
+            HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            ok = frame_of(c).ok;
+        }
+        c->last_sorted = ok;
+    }
     if (c->last_sorted) {
         int st = kv_copy_all(c);
         if (st) return st;
-        return apply_sorted(c, cols, c->segs, wall, d_event, out);
+        if (win_flags) {
+            if (n) HIPCHK(hipMemsetAsync(win_flags, 0, n, c->stream));
+            c->last_flagged = true;
+        }
+        return apply_sorted(c, cols, c->segs, wall, d_event, out, nullptr, win_flags);
     }
     return apply_ranges(c, cols, c->segs, n, mem, wall, d_event, win_flags, out);
 }
@@ -2550,6 +2647,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_NO_FUSE")) c->no_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
@@ -2625,6 +2723,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->p_plan.release(); c->p_l1beg.release(); c->h_pplan.release();
     c->p_ibase.release(); c->p_ksu32.release(); c->p_kslt.release(); c->p_tseg.release();
     c->p_ibucket.release();
+    c->f_pos1.release(); c->f_pos2.release(); c->f_flag1.release(); c->f_flag2.release();
+    c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
@@ -2931,10 +3031,10 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     if (c->timing) HIPCHK(ensure_events(c, events_for(R)));
     // the sorted path's packed form needs the records' frame: the scan reduces it on the way
     c->segs.from_offsets(batch->offsets, R);
-    const bool frame = !c->counts && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
+    const bool frame = (!c->counts || win_flags) && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
     c->last_anchored = false;
     PackFrame apf;
-    if (frame && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
+    if (frame && !win_flags && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
         (c->form_off & kFormAnchor) && anchored_frame(c, R, wall, &apf)) {
         if (c->anchor_skip) {
             --c->anchor_skip;
@@ -3006,6 +3106,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_key16) f |= CRDT_PLAN_KEY16;
         if (c->last_hw) f |= CRDT_PLAN_HIGH_WATER;
         if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
+        if (c->last_flagged) f |= CRDT_PLAN_FLAGGED;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;

@@ -244,8 +244,9 @@ int crdt_set_presharded(crdt_ctx* ctx, int presharded);
  * every record reads its row: K2) or by the sorted path (the applied records are
  * partitioned by key into 4096-key buckets, each bucket's rows are read and written
  * once and its records resolved in LDS; sorted_path.inc).  Both give identical
- * rows, canonical, status and counts.  The sorted path needs: win_flags == NULL,
- * canonical >= 0, capacity <= 2^28.  path: CRDT_PATH_AUTO (default, also set by the
+ * rows, canonical, status and counts.  The sorted path needs: canonical >= 0,
+ * capacity <= 2^28; with win_flags, also a single ctx and a batch frame that fits its 64-bit
+ * packed key (its flagged form), else the gather path runs.  path: CRDT_PATH_AUTO (default, also set by the
  * CRDT_MERGE_PATH environment variable = gather | sorted), CRDT_PATH_GATHER,
  * CRDT_PATH_SORTED (whenever allowed).  crdt_last_path reports the path the last
  * crdt_merge took (CRDT_PATH_GATHER or CRDT_PATH_SORTED). */
@@ -282,8 +283,10 @@ enum crdt_plan_flags {
                                     scan folded into the level-1 scatter */
     CRDT_PLAN_WIRE_PACKED = 256, /* sharded ctx: records crossed the all-to-all as 16-B packed
                                     {slot, (lt, rank, changeset) key, val} instead of 20 B */
-    CRDT_PLAN_OWN_IN_PLACE = 512 /* sharded ctx: the records this rank owns of its own batch were
+    CRDT_PLAN_OWN_IN_PLACE = 512, /* sharded ctx: the records this rank owns of its own batch were
                                     scattered straight into the receive columns (no device copy) */
+    CRDT_PLAN_FLAGGED = 1024     /* the sorted path's flagged form: per-record win flags (stable level 2,
+                                    ordered resolve, flags carried back to input order; sorted_path.inc) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

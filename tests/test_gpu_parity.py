@@ -1253,3 +1253,192 @@ def test_two_rank_routing_kernel_forms(gpu_device, monkeypatch, form_off):
               n_ranks=71, tomb_frac=0.1)
     run_shard_gpu(kw, 2, "routed", path="sorted", counts=False)
     run_shard_gpu(dict(CASE_SPECS)["drift_late"], 2, "routed")
+
+
+# ------------------------------------------------------------------ sorted path, flagged form
+# Per-record win flags on the sorted path (sorted_path.inc, "win flags"): stable level 2, the
+# ordered packed resolve, flags carried back to input order.  Every case against the oracle's
+# flags, rows, canonical, exception fields and exact counts (crdt.dart:80-90, map_crdt.dart:33-39).
+_TWO = (1 << 20) + 5
+
+
+def _flagged(case, capacity=None, **kw):
+    res = compare_with_oracle(case, path="sorted", flags=True, capacity=capacity, **kw)
+    return res
+
+
+@pytest.mark.parametrize("name", [n for n, _ in CASE_SPECS])
+@pytest.mark.parametrize("capacity", [None, _TWO])
+def test_flagged_golden_vectors(gpu_device, name, capacity):
+    """Every golden case with flags on a forced sorted path: the flagged form whenever the batch's
+    frame fits the packed key (else K2), same flags and counts as the golden outputs."""
+    case, exp, expected = golden_case(name)
+    rows, res, flags = device_run(case, path="sorted", flags=True, capacity=capacity)
+    check_rows(*rows, exp)
+    assert np.array_equal(flags, exp["flags"])
+    for k, v in expected.items():
+        assert res[k] == v, (name, k, res[k], v)
+    if res["path"] == "sorted":
+        assert res["plan"]["flagged"]
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("capacity", [None, _TWO])
+def test_flagged_random_small(gpu_device, seed, capacity):
+    rng = np.random.default_rng(1000 + seed)
+    kw = dict(seed=2000 + seed, R=int(rng.integers(1, 12)), per_cs=int(rng.integers(0, 500)),
+              n_local=int(rng.integers(1, 600)), n_new=int(rng.integers(0, 400)),
+              millis_span=int(rng.integers(1, 100)), counter_span=int(rng.integers(1, 8)),
+              n_ranks=int(rng.integers(2, 40)), tomb_frac=float(rng.random() * 0.5),
+              neg_mod_frac=float(rng.random() * 0.1), dup_frac=float(rng.random() * 0.01),
+              drift_frac=float(rng.random() * 0.005))
+    kw["local_rank"] = int(rng.integers(0, kw["n_ranks"]))
+    case = make_case(**kw)
+    res = _flagged(case, capacity)
+    if case["c0"] >= 0:
+        assert res["path"] == "sorted" and res["plan"]["flagged"], res["plan"]
+
+
+@pytest.mark.parametrize("capacity", [None, (1 << 20) + 7, 1 << 24])
+def test_flagged_ties_many_changesets(gpu_device, capacity):
+    """300 tie-heavy changesets: equal (lt, rank) across changesets (the earlier one wins, later
+    equal records do not), one- and two-level buckets."""
+    case = make_case(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8,
+                     counter_span=4, n_ranks=301)
+    res = _flagged(case, capacity)
+    assert res["path"] == "sorted" and res["plan"]["flagged"] and res["n_won"] > 0
+
+
+@pytest.mark.parametrize("capacity", [None, _TWO])
+def test_flagged_hot_keys_in_one_chunk(gpu_device, capacity):
+    """Dozens of records per key in every 2048-record chunk: long in-chunk same-key lists, the
+    left-to-right maxima decided inside the chunk."""
+    case = make_case(seed=83, R=400, per_cs=60, n_local=50, n_new=30, millis_span=3, counter_span=2,
+                     n_ranks=7)
+    res = _flagged(case, capacity)
+    assert res["path"] == "sorted" and res["plan"]["flagged"]
+
+
+@pytest.mark.parametrize("capacity", [None, _TWO])
+def test_flagged_split_hot_bucket(gpu_device, capacity):
+    """240K records in one 4096-key bucket: 4 parts (changeset ranges), each walked from its
+    carry-in (row folded with the earlier parts); ties and tombstones across the cuts."""
+    case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                     n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    res = _flagged(case, capacity)
+    assert res["path"] == "sorted" and res["plan"]["flagged"] and res["n_won"] > 0
+
+
+def test_flagged_split_buckets_across_blocks(gpu_device):
+    buckets = [3, 1023, 1024, 2047, 2048, 4095]
+    base = make_case(seed=86, R=40, per_cs=12_000, n_local=18_000, n_new=6 * 4096 - 18_000, millis_span=4,
+                     counter_span=3, n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    case = _spread_case(base, buckets, 1 << 24)
+    res = _flagged(case)
+    assert res["path"] == "sorted" and res["plan"]["flagged"] and res["n_won"] > 0
+
+
+def test_flagged_windows_and_late_exception(gpu_device):
+    """5000 changesets (two windows), a drift record in changeset 4500: the flags of changesets
+    from the stop on stay 0."""
+    case = make_case(seed=84, R=5000, per_cs=20, n_local=3000, n_new=2000, millis_span=20,
+                     force=[(4500, 7, "drift")])
+    res = _flagged(case)
+    assert res["status"] == 1 and res["exc_changeset"] == 4500 and res["path"] == "sorted"
+
+
+@pytest.mark.parametrize("seed", [91, 92])
+def test_flagged_frame_edges(gpu_device, seed):
+    """Local rows at every edge of the packed frame (below / at / above, ranks outside it, equal
+    (lt, rank) with a record), with and without a declared rank bound."""
+    case = _frame_edge_case(seed)
+    bound = int(case["rank"].max()) + 1
+    for cap in (None, (1 << 20) + 3):
+        for rb in (0, bound):
+            res = _flagged(case, cap, rank_bound=rb)
+            assert res["path"] == "sorted" and res["plan"]["flagged"]
+
+
+@pytest.mark.parametrize("cap", [None, _TWO])
+def test_flagged_late_drift(gpu_device, cap):
+    case = _late_drift_case(97)
+    res = _flagged(case, cap)
+    assert res["status"] == 1 and res["exc_changeset"] == 37 and res["plan"]["flagged"]
+
+
+@pytest.mark.parametrize("counts", [True, False])
+def test_flagged_cold_buckets(gpu_device, counts):
+    """Records spread thinly over many cold buckets of a > 2^20-key table (unsplit buckets at
+    level 2, 14/13-B records), counts on and off (the flagged form always counts)."""
+    case = _cold_bucket_case(95)
+    rows, res, flags = device_run(case, path="sorted", flags=True, counts=counts, capacity=case["n_ids"])
+    orows, ores, oflags = oracle_run(case)
+    assert res["plan"]["flagged"] and res["plan"]["key16"]
+    assert np.array_equal(flags, oflags)
+    for f, a in zip(("lt", "rank", "val", "mod"), rows):
+        assert np.array_equal(a, orows[f]), f
+    for k in RESULT_FIELDS:
+        assert res[k] == ores[k], (k, res[k], ores[k])
+
+
+def test_flagged_device_columns(gpu_device):
+    case = make_case(seed=88, R=90, per_cs=3000, n_local=9000, n_new=4000, millis_span=6, counter_span=3,
+                     n_ranks=11, tomb_frac=0.1)
+    res = compare_with_oracle(case, path="sorted", flags=True, capacity=_TWO, device_cols=True)
+    assert res["plan"]["flagged"]
+
+
+def test_flagged_key_out_of_range(gpu_device):
+    """A key id past the capacity: CRDT_E_KEY_RANGE, nothing stored, every flag 0."""
+    from crdt_amd import CrdtNativeError, DeviceTable
+    t = DeviceTable(0, local_rank=0, capacity=64)
+    t.set_merge_path("sorted")
+    with pytest.raises(CrdtNativeError):
+        t.merge(np.array([1, 10_000], np.uint32), np.array([5, 6], np.int64), np.array([1, 1], np.uint32),
+                np.array([0, 0], np.uint32), np.array([0, 2], np.uint64), 1 << 40, win_flags=True)
+    lt, rank, val, mod = t.read_rows(np.arange(64, dtype=np.uint32))
+    assert (mod < 0).all()
+    t.close()
+
+
+def test_flagged_switch_off(gpu_device, monkeypatch):
+    """CRDT_FLAGS_SORTED=0: a flagged merge takes K2, same results."""
+    monkeypatch.setenv("CRDT_FLAGS_SORTED", "0")
+    case = make_case(seed=89, R=70, per_cs=1000, n_local=3000, n_new=1000, millis_span=5)
+    res = _flagged(case)
+    assert res["path"] == "gather" and not res["plan"]["flagged"]
+
+
+@pytest.mark.parametrize("K,total,R", [(1 << 20, 3_000_000, 64), (1 << 24, 9_000_000, 96)])
+def test_flagged_equals_gather_fanin(gpu_device, K, total, R):
+    """A fan-in shape (Zipf keys, unique per replica, hot head split into parts) merged with flags on
+    both paths from the same state (auto picks the flagged form): same flags, rows, canonical, counts."""
+    import torch
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    own, loc = wl["owned"], wl["local"]
+    out = {}
+    auto = total >= (8 << 20)                  # auto takes the flagged form from 64 changesets / 8M records
+    for path in ("gather", None):
+        t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+        if path or not auto:
+            t.set_merge_path(path or "sorted")
+        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        t.canonical = wl["c0"]
+        res, fl = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                          win_flags=True)
+        assert t.last_path() == (path or "sorted")
+        if not path:
+            assert t.last_plan()["flagged"]
+        rows = t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))
+        out[path] = (res, fl.cpu().numpy(), rows)
+        t.close()
+    (rg, fg, ag), (rs, fs, as_) = out["gather"], out[None]
+    for k in RESULT_FIELDS:
+        assert rg[k] == rs[k], (k, rg[k], rs[k])
+    assert np.array_equal(fg, fs)
+    for a, b in zip(ag, as_):
+        assert np.array_equal(a, b)
+    torch.cuda.empty_cache()
