@@ -1522,8 +1522,9 @@ struct crdt_ctx {
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
     bool last_flagged = false;      // the last sorted apply was the flagged form
-    DBuf<uint32_t> f_pos1, f_pos2;  // level-1 position per input record, level-2 position per level-1 one
+    DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
     DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
+    DBuf<uint32_t> f_hist2, f_toff2; // level 2's tile histogram / offsets (level 1's stay for the flag pass)
     DBuf<unsigned long long> f_cin_key;   // split buckets: every part's carry-in
     DBuf<uint32_t> f_cin_val;
     DBuf<uint8_t> f_cin_pres;
@@ -2255,6 +2256,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             ev_record(c, kEvApply);
         }
         if (ph) ev_record(c, ev_window(2, false));
+        TileMap tm2f{};                              // level 2's tiling and counts (the flag pass)
+        uint32_t nt2f = 0;
+        const uint32_t* h2f = nullptr;
+        const uint32_t* t2f = nullptr;
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
@@ -2267,23 +2272,35 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             // then cover a short stretch of each level-1 bucket at a time
             const uint32_t ts2 = k16 && !(c->form_off & kFormNoHistW) && !(c->form_off & kFormBigTile2)
                                  ? (uint32_t)kPTile2 : (uint32_t)kPTile;
+            // (the flagged form keeps level 1's tile histogram and offsets for its flag pass: level 2
+            // counts into buffers of its own)
+            if (fl) {
+                HIPALLOC(c->f_hist2.ensure((size_t)nt2 * kDigits));
+                HIPALLOC(c->f_toff2.ensure((size_t)nt2 * kDigits));
+            }
+            uint32_t* h2p = fl ? c->f_hist2.p : c->p_hist.p;
+            uint32_t* t2p = fl ? c->f_toff2.p : c->p_toff.p;
+            h2f = h2p;
+            t2f = t2p;
             k_l2_plan<<<1, 256, 0, c->stream>>>(c->p_l1beg.p, tb2, cb2, ts2);
             k_seg_index<<<std::min<uint32_t>(grid_for(nt2, 256), 4096), 256, 0, c->stream>>>(tb2, kDigits, nt2,
                                                                                             c->p_tseg.p);
             const TileMap tm2{c->p_l1beg.p, c->p_l1beg.p + 1, tb2, c->p_tseg.p, nullptr, kDigits, ts2};
+            tm2f = tm2;
+            nt2f = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
             if (k16 && !(c->form_off & kFormNoHistW))   // key bits [4, 20) in 2 B: the level-2 digit
                 k_part_hist16w<<<nt2, kHThreads, 0, c->stream>>>(         // (bits [12, 20)) is its high byte
-                    reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, c->p_hist.p);
+                    reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, h2p);
             else if (k16)
                 k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap,
-                                                                          kSBits - 4, c->p_hist.p);
+                                                                          kSBits - 4, h2p);
             else
                 k_part_hist<false><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap, kSBits,
-                                                                      c->p_hist.p);
-            k_scan_part<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, sm2, c->p_part.p);
+                                                                      h2p);
+            k_scan_part<<<nc2, 256, 0, c->stream>>>(h2p, sm2, c->p_part.p);
             k_scan_seg<<<kDigits, 256, 0, c->stream>>>(c->p_part.p, sm2, c->p_choff.p, c->p_dstart2.p, nullptr);
-            k_scan_tiles<<<nc2, 256, 0, c->stream>>>(c->p_hist.p, c->p_choff.p, sm2, c->p_dstart2.p, c->p_toff.p);
+            k_scan_tiles<<<nc2, 256, 0, c->stream>>>(h2p, c->p_choff.p, sm2, c->p_dstart2.p, t2p);
             // (nt2 is an upper bound of the level-2 tiles; the real count is on the device)
             // (the grid and the XCD-contiguous mapping from a tile bound for THIS tile size: a loose
             // bound would leave the upper XCDs' ranges past the last tile, idle)
@@ -2293,29 +2310,29 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 HIPALLOC(c->f_pos2.ensure(nw));
                 if (k16)
                     k_part_scatter2<true, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                        p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
                 else if (k8)
                     k_part_scatter2<true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
                 else
                     k_part_scatter2<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
             } else if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
+                    p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
             else if (pk)
                 if (k16)
                     k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits - 4, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
+                        p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
                 else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
+                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
                 else
                     k_part_scatter2<false, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
+                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
             else
                 k_part_scatter2<false, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                    p1r, p1k, tm2, kSBits, c->p_toff.p, p2r, p2k, xper2, rev1 ? c->p_hist.p : nullptr);
+                    p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
         }
         if (ph) ev_record(c, ev_window(2, true));
         // resolve: items = parts of buckets (hot buckets split into kRPart-record parts)
@@ -2371,14 +2388,19 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint8_t* f1 = c->f_flag2.p;
             if (two) {
                 HIPALLOC(c->f_flag1.ensure(nw));
-                k_flags_back2<<<std::min<uint32_t>(grid_for(nw, 1024), 8192), 256, 0, c->stream>>>(
-                    c->f_pos2.p, c->f_flag2.p, c->p_l1beg.p + kDigits, c->d_misc, c->f_flag1.p);
+                if (k16)
+                    k_flags_back<false, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, kSBits - 4,
+                                                                          c->f_flag2.p, c->f_flag1.p, c->d_misc);
+                else
+                    k_flags_back<false, false><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, kSBits,
+                                                                           c->f_flag2.p, c->f_flag1.p, c->d_misc);
                 f1 = c->f_flag1.p;
                 // level 2 reused the tile -> segment index: rebuild level 1's
                 k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
                                                                                                  c->p_tseg.p);
             }
-            k_flags_back1<<<nt1, 1024, 0, c->stream>>>(tm1, c->d_misc, c->f_pos1.p, f1, dflags);
+            k_flags_back<true, false><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, cols.key,
+                                                                  shift1, f1, dflags, c->d_misc);
         } else if (c->counts) {
             k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                     c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
@@ -2725,6 +2747,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->p_ibucket.release();
     c->f_pos1.release(); c->f_pos2.release(); c->f_flag1.release(); c->f_flag2.release();
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
+    c->f_hist2.release(); c->f_toff2.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
