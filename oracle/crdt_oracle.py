@@ -35,6 +35,7 @@ reference test; they rest on the source reading of ``crdt.dart:82,86-87,93``.
 from __future__ import annotations
 
 import json
+import datetime as _dt
 import re
 
 SHIFT = 16                      # hlc.dart:3
@@ -75,91 +76,171 @@ def dart_compare(a, b) -> int:
 
 
 # ---------------------------------------------------------------------------
-# DateTime helpers (UTC) — the subset of dart:core the path touches [SDK]
+# DateTime helpers (UTC) — the subset of dart:core the path touches [SDK].
+# Written independently of crdt_amd/hlc.py (which uses the civil-from-days arithmetic and a
+# regular expression): calendar maths through Python's datetime.date ordinals, shifted by whole
+# 400-year Gregorian cycles for years outside 1..9999, and a character scanner for the grammar.
 # ---------------------------------------------------------------------------
-_DAYS_BEFORE_MONTH = [0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334]
+_EPOCH_ORDINAL = _dt.date(1970, 1, 1).toordinal()
+_CYCLE_DAYS = 146097                    # days in 400 Gregorian years (the calendar repeats)
+_MAX_ORDINAL = _dt.date.max.toordinal()
+_MAX_MS = 8640000000000000              # DateTime's range: +-10^8 days
 
 
-def _is_leap(y: int) -> bool:
-    return y % 4 == 0 and (y % 100 != 0 or y % 400 == 0)
+def _ymd_from_epoch_days(days: int):
+    """(year, month, day) of a day count since 1970-01-01, any year."""
+    o = days + _EPOCH_ORDINAL
+    cycles = 0
+    if o < 1:
+        cycles = -((1 - o + _CYCLE_DAYS - 1) // _CYCLE_DAYS)
+    elif o > _MAX_ORDINAL:
+        cycles = (o - _MAX_ORDINAL + _CYCLE_DAYS - 1) // _CYCLE_DAYS
+    d = _dt.date.fromordinal(o - cycles * _CYCLE_DAYS)
+    return d.year + 400 * cycles, d.month, d.day
 
 
-def _days_from_civil(y: int, m: int, d: int) -> int:
-    """Days since 1970-01-01 (proleptic Gregorian), m in 1..12."""
-    y -= m <= 2
-    era = y // 400
-    yoe = y - era * 400
-    mp = (m + 9) % 12
-    doy = (153 * mp + 2) // 5 + d - 1
-    doe = yoe * 365 + yoe // 4 - yoe // 100 + doy
-    return era * 146097 + doe - 719468
-
-
-def _civil_from_days(z: int):
-    z += 719468
-    era = z // 146097
-    doe = z - era * 146097
-    yoe = (doe - doe // 1460 + doe // 36524 - doe // 146096) // 365
-    y = yoe + era * 400
-    doy = doe - (365 * yoe + yoe // 4 - yoe // 100)
-    mp = (5 * doy + 2) // 153
-    d = doy - (153 * mp + 2) // 5 + 1
-    m = mp + 3 if mp < 10 else mp - 9
-    return y + (m <= 2), m, d
-
-
-_MAX_MS = 8640000000000000
+def _epoch_days(year: int, month: int, day: int) -> int:
+    """Days since 1970-01-01 of year-month-1 plus day - 1 (day may overflow the month, as DateTime
+    normalises it); month in 1..12, any year."""
+    cycles = 0
+    if year < 1:
+        cycles = -((1 - year + 399) // 400)
+    elif year > 9999:
+        cycles = (year - 9999 + 399) // 400
+    first = _dt.date(year - 400 * cycles, month, 1).toordinal()
+    return first - _EPOCH_ORDINAL + cycles * _CYCLE_DAYS + day - 1
 
 
 def iso_from_millis(ms: int) -> str:
     """``DateTime.fromMillisecondsSinceEpoch(ms, isUtc: true).toIso8601String()``."""
     if abs(ms) > _MAX_MS:
         raise ValueError(f"RangeError: {ms}")
-    days, rem = divmod(ms, 86400000)
-    y, mo, d = _civil_from_days(days)
-    h, rem = divmod(rem, 3600000)
-    mi, rem = divmod(rem, 60000)
-    s, milli = divmod(rem, 1000)
-    if -9999 <= y <= 9999:
-        ys = ("-" if y < 0 else "") + str(abs(y)).rjust(4, "0")
+    days = ms // 86400000
+    in_day = ms - days * 86400000
+    y, mo, d = _ymd_from_epoch_days(days)
+    t = _dt.time(in_day // 3600000, in_day // 60000 % 60, in_day // 1000 % 60, in_day % 1000 * 1000)
+    if abs(y) <= 9999:
+        year = ("-%04d" % -y) if y < 0 else "%04d" % y
     else:
-        ys = ("-" if y < 0 else "+") + str(abs(y)).rjust(6, "0")
-    return f"{ys}-{mo:02d}-{d:02d}T{h:02d}:{mi:02d}:{s:02d}.{milli:03d}Z"
+        year = ("-%06d" % -y) if y < 0 else "+%06d" % y
+    return "%s-%02d-%02dT%s.%03dZ" % (year, mo, d, t.strftime("%H:%M:%S"), t.microsecond // 1000)
 
 
-_PARSE_RE = re.compile(
-    r"^([+-]?\d{4,6})-?(\d\d)-?(\d\d)"
-    r"(?:[ T](\d\d)(?::?(\d\d)(?::?(\d\d)(?:[.,](\d+))?)?)?"
-    r"( ?[zZ]| ?([-+])(\d\d)(?::?(\d\d))?)?)?$")
+class _Scan:
+    """A cursor over the date string (DateTime.parse's grammar, scanned by hand)."""
+
+    def __init__(self, s: str):
+        self.s, self.i = s, 0
+
+    def peek(self, chars: str) -> bool:
+        return self.i < len(self.s) and self.s[self.i] in chars
+
+    def take(self, chars: str) -> str:
+        if self.peek(chars):
+            self.i += 1
+            return self.s[self.i - 1]
+        return ""
+
+    def digits(self, lo: int, hi: int):
+        j = self.i
+        while j < len(self.s) and j - self.i < hi and "0" <= self.s[j] <= "9":
+            j += 1
+        if j - self.i < lo:
+            return None
+        out = int(self.s[self.i:j])
+        self.i = j
+        return out
+
+    def run_of_digits(self) -> str:
+        j = self.i
+        while j < len(self.s) and "0" <= self.s[j] <= "9":
+            j += 1
+        out = self.s[self.i:j]
+        self.i = j
+        return out
 
 
 def millis_from_iso(s: str) -> int:
-    """``DateTime.parse(s).millisecondsSinceEpoch`` (zone-less strings read as UTC)."""
-    m = _PARSE_RE.match(s)
-    if not m:
-        raise ValueError(f"FormatException: Invalid date format {s}")
-    year = int(m.group(1))
-    month = int(m.group(2))
-    day = int(m.group(3))
-    hour = int(m.group(4) or 0)
-    minute = int(m.group(5) or 0)
-    second = int(m.group(6) or 0)
-    frac = m.group(7)
-    micros = 0
-    if frac:
-        digits = (frac + "000000")[:6]
-        micros = int(digits)
-    # month overflow normalisation as DateTime does (month is two digits here)
-    mz = month - 1
-    year += mz // 12
-    mz %= 12
-    days = _days_from_civil(year, mz + 1, 1) + day - 1
-    total_us = ((days * 24 + hour) * 60 + minute) * 60 + second
+    """``DateTime.parse(s).millisecondsSinceEpoch`` (zone-less strings read as UTC).  The year takes
+    4 to 6 digits: the longest that lets the rest of the string parse (a compact "20010909T..."
+    has a 4-digit year)."""
+    bad = ValueError(f"FormatException: Invalid date format {s}")
+    for ylen in (6, 5, 4):
+        try:
+            return _millis_from_iso(s, ylen, bad)
+        except _NoParse:
+            continue
+    raise bad
+
+
+class _NoParse(Exception):
+    pass
+
+
+def _millis_from_iso(s: str, ylen: int, bad: ValueError) -> int:
+    c = _Scan(s)
+    sign = c.take("+-")
+    year = c.digits(ylen, ylen)
+    if year is None:
+        raise _NoParse
+    year = -year if sign == "-" else year
+    c.take("-")
+    month = c.digits(2, 2)
+    c.take("-")
+    day = c.digits(2, 2)
+    if month is None or day is None:
+        raise _NoParse
+    hour = minute = second = micros = 0
+    zone = None
+    if c.take(" T"):
+        hour = c.digits(2, 2)
+        if hour is None:
+            raise _NoParse
+        save = c.i
+        c.take(":")
+        mm = c.digits(2, 2)
+        if mm is None:
+            c.i = save
+        else:
+            minute = mm
+            save = c.i
+            c.take(":")
+            ss = c.digits(2, 2)
+            if ss is None:
+                c.i = save
+            else:
+                second = ss
+                if c.take(".,"):
+                    frac = c.run_of_digits()
+                    if not frac:
+                        raise _NoParse
+                    micros = int(frac[:6].ljust(6, "0"))
+        save = c.i
+        c.take(" ")
+        if c.take("zZ"):
+            zone = 0
+        elif c.peek("+-"):
+            zsign = -1 if c.take("+-") == "-" else 1
+            zh = c.digits(2, 2)
+            if zh is None:
+                raise _NoParse
+            save2 = c.i
+            c.take(":")
+            zm = c.digits(2, 2)
+            if zm is None:
+                c.i = save2
+                zm = 0
+            zone = zsign * (zh * 60 + zm)
+        else:
+            c.i = save
+    if c.i != len(s):
+        raise _NoParse
+    year += (month - 1) // 12                 # month overflow, as DateTime normalises it
+    month = (month - 1) % 12 + 1
+    total_us = ((_epoch_days(year, month, day) * 24 + hour) * 60 + minute) * 60 + second
     total_us = total_us * 1000000 + micros
-    if m.group(8) is not None and m.group(9) is not None:
-        sign = -1 if m.group(9) == "-" else 1
-        off = int(m.group(10)) * 60 + int(m.group(11) or 0)
-        total_us -= sign * off * 60 * 1000000
+    if zone:
+        total_us -= zone * 60 * 1000000
     ms = _trunc_div(total_us, 1000)
     if abs(ms) > _MAX_MS:
         raise ValueError(f"FormatException: Time out of range {s}")

@@ -184,3 +184,28 @@ def test_workload_generators_cpu():
     for j in range(16):
         k = wl3["owned"]["key"][int(o3[j]):int(o3[j + 1])]
         assert torch.unique(k).numel() == k.numel()
+
+
+def test_iso_edge_strings_match_independent_oracle():
+    """The oracle's date maths (datetime ordinals + 400-year shifts, a hand-written scanner) is
+    independent of crdt_amd/hlc.py's (civil-from-days, regular expression): they must agree on
+    DateTime's whole range and on the grammar's edges, errors included."""
+    from oracle.crdt_oracle import iso_from_millis as o_iso, millis_from_iso as o_parse
+    rng = np.random.default_rng(7)
+    edges = [8640000000000000, -8640000000000000, -62135596800001, -62135596800000, 253402300800000]
+    for ms in [int(x) for x in rng.integers(-8640000000000000, 8640000000000000, 3000)] + edges:
+        assert iso_from_millis(ms) == o_iso(ms)
+        assert millis_from_iso(o_iso(ms)) == ms
+    strings = ["2001-09-09T01:46:40Z", "20010909T014640", "+002001-01-01", "-0001-12-31T23:59:59.999Z",
+               "2020-02-31", "2001-13-01", "2001-09-09T01:46", "2001-09-09T01", "2001-09-09T0146Z",
+               "2001-09-09T01:46:40,5-0130", "2001-09-09T01:46:40 Z", "275760-09-13T00:00:00Z",
+               "-271821-04-20T00:00:00Z", "2001-9-09", "abc", "2001-09-09T", "2001-09-09T01:4",
+               "2001-09-09T01:46:40.", "1234567-01-01", "275760-09-13T00:00:00.001Z"]
+    for s in strings:
+        got = []
+        for f in (millis_from_iso, o_parse):
+            try:
+                got.append(f(s))
+            except ValueError:
+                got.append("error")
+        assert got[0] == got[1], (s, got)
