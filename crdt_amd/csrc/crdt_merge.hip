@@ -1521,7 +1521,9 @@ struct crdt_ctx {
     // per-record win flags on the sorted path (the flagged form, sorted_path.inc): CRDT_FLAGS_SORTED=0
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
+    int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
     bool last_flagged = false;      // the last sorted apply was the flagged form
+    bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
     DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
     DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
     DBuf<uint32_t> f_hist2, f_toff2; // level 2's tile histogram / offsets (level 1's stay for the flag pass)
@@ -2083,7 +2085,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     if (anchor) {
         pf = *anchor;
         pk = true;
-    } else if (cols.packed_in || ((!c->counts || fl) && c->packed_resolve && c->frame_on)) {
+    } else if (cols.packed_in || (c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         pf = frame_of(c);
@@ -2091,6 +2093,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
     if (fl && (!pk || anchor || cols.packed_in)) return CRDT_E_INVALID;      // apply_segs checked the frame
+    // the ordered packed form: the flagged form's kernels, for win flags and / or exact per-record
+    // counts (without flags: no positions kept, no flags carried back)
+    const bool ord = fl || (c->counts && pk && !anchor && !cols.packed_in);
+    c->last_ordered = ord;
     c->last_packed = pk;
     c->key_end_valid = true;                 // k_bucket_items bounds the rows every window writes
     c->last_hist1_fused = false;
@@ -2100,7 +2106,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
     c->last_key8 = k8;
     c->last_key16 = k16;
-    c->last_hw = pk && (!c->counts || fl) && c->hw_read < c->cap;     // (in the first window)
+    c->last_hw = pk && (!c->counts || ord) && c->hw_read < c->cap;     // (in the first window)
     if (fl) {
         uint64_t ncol = 0;                                           // input index space of pos1
         for (size_t s = 0; s < ns_all; ++s) ncol = std::max<uint64_t>(ncol, sg.end[s]);
@@ -2306,17 +2312,21 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             // bound would leave the upper XCDs' ranges past the last tile, idle)
             const uint32_t nt2s = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const uint32_t xper2 = c->xcd_map ? (nt2s + kXcds - 1) / kXcds : 0;
-            if (fl) {          // stable: each final bucket in changeset order; level-2 positions kept
-                HIPALLOC(c->f_pos2.ensure(nw));
+            if (ord) {         // changeset order kept in every final bucket; level-2 run offsets kept
+                if (fl) HIPALLOC(c->f_pos2.ensure(nw));
+                uint16_t* pos2 = fl ? c->f_pos2.p : nullptr;
+                const Rec12* i12 = reinterpret_cast<const Rec12*>(p1r);
+                Rec12* o12 = reinterpret_cast<Rec12*>(p2r);
+                const uint32_t jm = (uint32_t)pack_jmask(pf);
                 if (k16)
-                    k_part_scatter2<true, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                    k_part_scatter2_seg<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        i12, p1k, tm2, kSBits - 4, t2p, o12, p2k, xper2, jm, pos2);
                 else if (k8)
-                    k_part_scatter2<true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                    k_part_scatter2_seg<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2);
                 else
-                    k_part_scatter2<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, nullptr, c->f_pos2.p);
+                    k_part_scatter2_seg<false, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2);
             } else if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
@@ -2356,14 +2366,15 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
-        if (fl) {          // the ordered packed resolve with flags (sorted_path.inc, "win flags")
+        if (ord) {         // the ordered packed resolve: flags and / or counts (sorted_path.inc, "win flags")
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
             HIPALLOC(c->f_cin_key.ensure(ksn));
             HIPALLOC(c->f_cin_val.ensure(ksn));
             HIPALLOC(c->f_cin_pres.ensure(ksn));
-            HIPALLOC(c->f_flag2.ensure(nw));
+            if (fl) HIPALLOC(c->f_flag2.ensure(nw));
+            uint8_t* fl2 = fl ? c->f_flag2.p : nullptr;
             if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
@@ -2376,17 +2387,19 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
                 reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
-            if (k8)
-                k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
-                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, c->f_flag2.p);
-            else
-                k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
-                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, c->f_flag2.p);
+#define CRDT_PFLAGS(K8, T)                                                                                  \
+    k_resolve_pflags<K8, T><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv,   \
+                                                            c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,  \
+                                                            c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2)
+            if (c->pf_threads == 512) {
+                if (k8) CRDT_PFLAGS(true, 512); else CRDT_PFLAGS(false, 512);
+            } else {
+                if (k8) CRDT_PFLAGS(true, 1024); else CRDT_PFLAGS(false, 1024);
+            }
+#undef CRDT_PFLAGS
             // flags back: level-2 order -> level-1 order (two levels) -> input order
             const uint8_t* f1 = c->f_flag2.p;
-            if (two) {
+            if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw));
                 if (k16)
                     k_flags_back<false, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, kSBits - 4,
@@ -2399,6 +2412,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
                                                                                                  c->p_tseg.p);
             }
+            if (fl)
             k_flags_back<true, false><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, cols.key,
                                                                   shift1, f1, dflags, c->d_misc);
         } else if (c->counts) {
@@ -2670,6 +2684,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
@@ -3054,10 +3069,10 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     if (c->timing) HIPCHK(ensure_events(c, events_for(R)));
     // the sorted path's packed form needs the records' frame: the scan reduces it on the way
     c->segs.from_offsets(batch->offsets, R);
-    const bool frame = (!c->counts || win_flags) && c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
+    const bool frame = c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
     c->last_anchored = false;
     PackFrame apf;
-    if (frame && !win_flags && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
+    if (frame && !win_flags && !c->counts && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
         (c->form_off & kFormAnchor) && anchored_frame(c, R, wall, &apf)) {
         if (c->anchor_skip) {
             --c->anchor_skip;
@@ -3130,6 +3145,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_hw) f |= CRDT_PLAN_HIGH_WATER;
         if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
         if (c->last_flagged) f |= CRDT_PLAN_FLAGGED;
+        if (c->last_ordered) f |= CRDT_PLAN_ORDERED;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;

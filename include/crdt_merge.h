@@ -285,8 +285,9 @@ enum crdt_plan_flags {
                                     {slot, (lt, rank, changeset) key, val} instead of 20 B */
     CRDT_PLAN_OWN_IN_PLACE = 512, /* sharded ctx: the records this rank owns of its own batch were
                                     scattered straight into the receive columns (no device copy) */
-    CRDT_PLAN_FLAGGED = 1024     /* the sorted path's flagged form: per-record win flags (stable level 2,
-                                    ordered resolve, flags carried back to input order; sorted_path.inc) */
+    CRDT_PLAN_FLAGGED = 1024,    /* the sorted path's flagged form: per-record win flags (changeset-ordered
+                                    level 2, ordered resolve, flags carried back to input order; sorted_path.inc) */
+    CRDT_PLAN_ORDERED = 2048     /* ... its ordered packed resolve (flags and / or exact n_present / n_won) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

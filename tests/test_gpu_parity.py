@@ -720,20 +720,16 @@ def test_sorted_hist_in_scan(gpu_device, monkeypatch, kind, cap):
 
 @pytest.mark.parametrize("counts", [False, True])
 def test_rank_bound_violation_stores_nothing(gpu_device, counts):
-    """A batch rank at or above the promised bound: the packed sorted form refuses the call with
-    CRDT_E_INVALID before writing a row (canonical unchanged); the counted form does not use the
-    bound and merges exactly."""
+    """A batch rank at or above the promised bound: the packed sorted forms (order-free, and the
+    ordered one exact counts take) refuse the call with CRDT_E_INVALID before writing a row
+    (canonical unchanged); with the promise withdrawn the batch merges exactly."""
     from crdt_amd import CrdtNativeError, DeviceTable
     case = make_case(seed=94, R=20, per_cs=1000, n_local=2000, n_new=500, millis_span=4, counter_span=2,
                      n_ranks=9, tomb_frac=0.1)
     bound = int(case["rank"].max())               # the highest rank breaks the promise
-    if counts:
-        res = compare_with_oracle(case, path="sorted", flags=False, counts=True, rank_bound=bound)
-        assert res["status"] == 0
-        return
     t = DeviceTable(0, local_rank=case["local_rank"], capacity=case["n_ids"])
     t.set_merge_path("sorted")
-    t.set_counts(False)
+    t.set_counts(counts)
     t.set_rank_bound(bound)
     loc = case["local"]
     keep = loc["mod"] != ABSENT_MOD
