@@ -2502,8 +2502,10 @@ bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* wi
     // auto: a many-changeset fan-in.  Order-free (no per-record counts): the partitioned passes
     // beat R K2 launches from 64 changesets and 8M records on (1B fan-in: 31.4 vs 34.1 ms,
     // DESIGN.md §5); with exact counts only while changesets are small (cfg3), where K2's
-    // launches are latency-bound; the flagged form counts exactly (its resolve walks in order)
-    return R >= 64 && n >= (8ull << 20) && (win_flags || !c->counts || n / R <= (256ull << 10));
+    // launches are latency-bound; the ordered packed form counts exactly (its resolve walks in
+    // order) and serves flags — apply_segs sends a batch whose frame does not fit it to K2
+    return R >= 64 && n >= (8ull << 20) &&
+           (win_flags || !c->counts || c->packed_resolve || n / R <= (256ull << 10));
 }
 
 // Apply phase over columns whose changeset segments are c->segs (n = column length).
@@ -2512,8 +2514,11 @@ int apply_segs(crdt_ctx* c, const Cols& cols, uint64_t n, int32_t mem, int64_t w
     if (c->timing) HIPCHK(ensure_events(c, events_for(c->segs.j.size())));
     c->last_sorted = allow_sorted && use_sorted(c, c->segs, c->plan_R, win_flags);
     c->last_flagged = false;
-    if (c->last_sorted && win_flags) {
-        // the flagged form runs on the packed key: the scan's frame must fit it (else K2)
+    // flags, or exact counts on large changesets (admitted for the ordered packed form): the scan's
+    // frame must fit the packed key, else K2
+    const uint64_t nrec = c->segs.j.empty() ? 0 : n;
+    const bool big_cs = c->counts && c->merge_path != 2 && c->plan_R && nrec / c->plan_R > (256ull << 10);
+    if (c->last_sorted && (win_flags || big_cs)) {
         bool ok = mem == CRDT_MEM_DEVICE && c->frame_on && !cols.packed_in;
         if (ok) {
             HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
