@@ -1522,6 +1522,7 @@ struct crdt_ctx {
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
+    bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     bool last_flagged = false;      // the last sorted apply was the flagged form
     bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
     DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
@@ -2388,13 +2389,16 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
 #define CRDT_PFLAGS(K8, T)                                                                                  \
-    k_resolve_pflags<K8, T><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv,   \
+    if (c->pf_head32) k_resolve_pflags<K8, T, true><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb,           \
+        c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink, c->f_cin_val.p,        \
+        c->f_cin_pres.p, pf, c->d_misc, fl2);                                                                   \
+    else k_resolve_pflags<K8, T><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, \
                                                             c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,  \
                                                             c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2)
             if (c->pf_threads == 512) {
-                if (k8) CRDT_PFLAGS(true, 512); else CRDT_PFLAGS(false, 512);
+                if (k8) { CRDT_PFLAGS(true, 512); } else { CRDT_PFLAGS(false, 512); }
             } else {
-                if (k8) CRDT_PFLAGS(true, 1024); else CRDT_PFLAGS(false, 1024);
+                if (k8) { CRDT_PFLAGS(true, 1024); } else { CRDT_PFLAGS(false, 1024); }
             }
 #undef CRDT_PFLAGS
             // flags back: level-2 order -> level-1 order (two levels) -> input order
@@ -2690,6 +2694,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
+    if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);

@@ -1,0 +1,27 @@
+#!/bin/bash
+# SQ counters of the flagged form's kernels beside the order-free ones (tools/prof_flags.py with MIX=1:
+# steps alternate flags / no flags), one --pmc pass.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+rm -rf gpurun_out/pmc_flags_sq
+MIX=1 STEPS=4 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_flags_sq -o run -- python3 tools/prof_flags.py > gpurun_out/pmc_flags_sq.log 2>&1
+rc=$?; echo "[pmc] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_flags_sq.log; exit $rc; }
+python3 - <<'PY'
+import csv, glob, collections
+f = glob.glob("gpurun_out/pmc_flags_sq/**/*counter_collection.csv", recursive=True)[0]
+acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
+for r in csv.DictReader(open(f)):
+    k = r["Kernel_Name"]
+    if "k_" not in k: continue
+    k = k.split("(")[0].replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+    acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    n[(k, r["Counter_Name"])] += 1
+for k, c in acc.items():
+    if c.get("SQ_WAVE_CYCLES", 0) < 1e8: continue
+    w = c["SQ_WAVE_CYCLES"]
+    print(f"{k[:60]:60s} waitany {c['SQ_WAIT_ANY']/w:.2f} waitlds {c['SQ_WAIT_INST_LDS']/w:.2f} "
+          f"ldsconf/ldsinst {c['SQ_LDS_BANK_CONFLICT']/max(c['SQ_INSTS_LDS'],1):.2f} "
+          f"lds/valu {c['SQ_INSTS_LDS']/max(c['SQ_INSTS_VALU'],1):.2f} valu {c['SQ_INSTS_VALU']:.3g} lds {c['SQ_INSTS_LDS']:.3g}")
+PY

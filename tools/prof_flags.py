@@ -29,7 +29,8 @@ for i in range(steps):
     t.canonical = wl["c0"]
     torch.cuda.synchronize()
     ts = time.perf_counter()
-    res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"], win_flags=flags)
+    fl = flags if not (os.environ.get("MIX") and i % 2) else False      # MIX=1: odd steps without flags
+    res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"], win_flags=fl)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - ts) * 1e3
     tag = os.environ.get(ab_var) if ab else ""
