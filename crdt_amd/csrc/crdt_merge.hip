@@ -1524,6 +1524,11 @@ struct crdt_ctx {
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     bool last_flagged = false;      // the last sorted apply was the flagged form
+    bool combine = true;            // sharded order-free merges fold home records before routing (CRDT_COMBINE=0: off)
+    bool last_combined = false;
+    DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
+    DBuf<uint64_t> e_pk;
+    DBuf<unsigned long long> e_cnt, e_cur;
     bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
     DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
     DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
@@ -2064,18 +2069,24 @@ void prof_resolve_report() {
 // (tile maxima from the level-1 scatter, recurrence, exception scan, stop point) run between the
 // level-1 scatter and level 2 instead of before this function.
 int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
-                 crdt_result* out, const PackFrame* anchor = nullptr, uint8_t* dflags = nullptr) {
+                 crdt_result* out, const PackFrame* anchor = nullptr, uint8_t* dflags = nullptr,
+                 const EmitOut* emit = nullptr) {
     const uint32_t R = c->plan_R;
     // dflags (device, zeroed by the caller): the flagged form — packed records, stable level 2, the
     // ordered resolve with per-record flags, and the flags carried back to input order
     const bool fl = dflags != nullptr;
-    if (!c->resolved && !anchor)
-        k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
-    c->resolved = false;
-    if (!anchor) ev_record(c, kEvApply);
-    c->windows.clear();
-    c->apply_total = 1;
-    if (c->timing) ev_record(c, ev_window(0, false));
+    // emit (comm_path.inc, map-side combine): fold the records against an absent table (the caller sets
+    // the key range and hw_read = 0) and emit one packed maximum per key; no row, result or timing
+    const bool em = emit != nullptr;
+    if (!em) {
+        if (!c->resolved && !anchor)
+            k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
+        c->resolved = false;
+        if (!anchor) ev_record(c, kEvApply);
+        c->windows.clear();
+        c->apply_total = 1;
+        if (c->timing) ev_record(c, ev_window(0, false));
+    }
     const bool two = c->cap > (1ull << 20);
     const uint32_t shift1 = two ? 20u : (uint32_t)kSBits;
     const size_t ns_all = sg.j.size();
@@ -2093,10 +2104,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         pk = pf.ok;
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
-    if (fl && (!pk || anchor || cols.packed_in)) return CRDT_E_INVALID;      // apply_segs checked the frame
+    if ((fl || em) && (!pk || anchor || cols.packed_in)) return CRDT_E_INVALID;   // the callers checked the frame
     // the ordered packed form: the flagged form's kernels, for win flags and / or exact per-record
     // counts (without flags: no positions kept, no flags carried back)
-    const bool ord = fl || (c->counts && pk && !anchor && !cols.packed_in);
+    const bool ord = !em && (fl || (c->counts && pk && !anchor && !cols.packed_in));
     c->last_ordered = ord;
     c->last_packed = pk;
     c->key_end_valid = true;                 // k_bucket_items bounds the rows every window writes
@@ -2194,7 +2205,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_scan_seg<<<1, 256, 0, c->stream>>>(c->p_part.p, sm1, c->p_choff.p, c->p_dstart1.p,
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
-        const bool ph = c->timing && s0 == 0;       // phase events: the first window
+        const bool ph = c->timing && s0 == 0 && !em;   // phase events: the first window
         if (anchor) ev_record(c, kEvScan);          // (anchored: the keys-only histogram pass and its scans)
         if (ph) ev_record(c, ev_window(1, false));
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
@@ -2367,7 +2378,28 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
-        if (ord) {         // the ordered packed resolve: flags and / or counts (sorted_path.inc, "win flags")
+        if (em) {          // map-side combine: part folds, then every key's maximum emitted
+            uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
+            uint32_t* ps_val = c->p_ksu32.p;
+            const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
+            if (k8) {
+                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, 0, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc);
+                k_resolve_packed<false, false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, 0, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, *emit);
+            } else {
+                k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, 0, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc);
+                k_resolve_packed<false, false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, 0, c->d_Rj.p, jb, ps_key, ps_val,
+                    pf, c->d_misc, *emit);
+            }
+            k_part_carry_packed<true><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+                d_hot, d_ib, d_hb, c->table, c->cap, 0, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc, *emit);
+        } else if (ord) {  // the ordered packed resolve: flags and / or counts (sorted_path.inc, "win flags")
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
@@ -2438,7 +2470,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
-            k_part_carry_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+            k_part_carry_packed<false><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
                 k_resolve_packed<false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
@@ -2475,6 +2507,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         // the next window reads rows this one may have written anywhere below the capacity
         c->hw_read = c->cap;
     }
+    if (em) return CRDT_OK;
     if (c->timing) {
         ev_record(c, ev_window(0, true));
         c->windows.push_back(1u);
@@ -2693,6 +2726,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_COMBINE")) c->combine = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
@@ -2773,6 +2807,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_pos1.release(); c->f_pos2.release(); c->f_flag1.release(); c->f_flag2.release();
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     c->f_hist2.release(); c->f_toff2.release();
+    c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
@@ -3156,6 +3191,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
         if (c->last_flagged) f |= CRDT_PLAN_FLAGGED;
         if (c->last_ordered) f |= CRDT_PLAN_ORDERED;
+        if (c->last_combined) f |= CRDT_PLAN_COMBINED;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;

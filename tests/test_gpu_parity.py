@@ -383,22 +383,50 @@ def test_two_rank_routed_sorted_path(gpu_device, counts):
 @pytest.mark.parametrize("kind", ["routed", "parts"])
 @pytest.mark.parametrize("path", ["gather", "sorted"])
 @pytest.mark.parametrize("name", ["r8_tombstones", "drift_late", "explicit_millis"])
-def test_two_rank_own_chunk_in_place(gpu_device, name, kind, path):
+def test_two_rank_own_chunk_in_place(gpu_device, monkeypatch, name, kind, path):
     """The second collective merge on each ctx scatters the rank's own chunk straight into the
     receive columns (sized by the first call; CRDT_PLAN_OWN_IN_PLACE): every shard row, canonical and
-    exception fields vs the oracle, gather and sorted receivers (win flags keep the copy)."""
+    exception fields vs the oracle, gather and sorted receivers (win flags keep the copy).  The
+    map-side combine is off here (CRDT_COMBINE=0): it routes folded keys, not records."""
+    monkeypatch.setenv("CRDT_COMBINE", "0")
     outs = run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path=path, counts=path == "gather", again=True)
     for rank, res, *_ in outs:
         assert res["plan"]["own_in_place"] == (path != "gather"), (rank, res["plan"])
+        assert not res["plan"]["combined"]
 
 
 @pytest.mark.parametrize("kind", ["routed", "parts"])
 @pytest.mark.parametrize("name", ["r4_ties", "drift_late", "send_overflow", "explicit_millis"])
-def test_two_rank_packed_wire_gather_receiver(gpu_device, name, kind):
+def test_two_rank_packed_wire_gather_receiver(gpu_device, monkeypatch, name, kind):
     """Order-free merge without win flags: the global frame fits, so records cross as 16-B packed
     {slot, key, val}; these batches are small, so each owner applies them on the gather path and
-    unpacks (lt, rank) first (k_unpack_routed)."""
+    unpacks (lt, rank) first (k_unpack_routed).  (The map-side combine off: with it on, owners
+    always resolve on the sorted path — test_two_rank_combine.)"""
+    monkeypatch.setenv("CRDT_COMBINE", "0")
     run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path="auto", counts=False)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["routed", "parts"])
+@pytest.mark.parametrize("name", ["r4_ties", "r8_tombstones", "drift_late", "dup_node", "send_overflow",
+                                  "explicit_millis"])
+def test_two_rank_combine(gpu_device, name, kind, world):
+    """The map-side combine (order-free, frame fits): each rank folds its home records into one
+    packed maximum per key (apply_sorted's emit mode), routes those, and the owners resolve them on
+    the sorted path — every shard row, canonical and exception fields vs the oracle."""
+    outs = run_shard_gpu(dict(CASE_SPECS)[name], world, kind, path="auto", counts=False)
+    for rank, res, *_ in outs:
+        if res["status"] == 0 or res["plan"]["combined"]:
+            assert res["plan"]["combined"] == res["plan"]["wire_packed"], (rank, res["plan"])
+
+
+def test_two_rank_combine_hot_and_windows(gpu_device):
+    """Combine with split (hot) buckets on the home fold and on the owners: 240K records over 4096
+    keys in 120 changesets, ties and tombstones, 2 ranks."""
+    kw = dict(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+              n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    outs = run_shard_gpu(kw, 2, "routed", path="auto", counts=False)
+    assert all(o[1]["plan"]["combined"] for o in outs), [o[1]["plan"] for o in outs]
 
 
 @pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
@@ -447,9 +475,12 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R):
         dist.destroy_process_group()
 
 
-def test_two_rank_routed_fanin_equals_one_gpu(gpu_device):
+@pytest.mark.parametrize("combine", ["1", "0"])
+def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine):
     """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
-    routed to key % 2) give exactly the rows and canonical of the unsharded merge."""
+    routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
+    map-side combine (each rank folds its home records per key before the exchange) and without."""
+    monkeypatch.setenv("CRDT_COMBINE", combine)
     import torch.multiprocessing as mp
 
     from crdt_amd import DeviceTable
@@ -494,19 +525,24 @@ def test_eight_rank_routed_small(gpu_device, name):
     assert all(o[1]["path"] in ("sorted", "gather") for o in outs)
 
 
+@pytest.mark.parametrize("combine", ["1", "0"])
 @pytest.mark.parametrize("inject", [None, "drift", "dup"])
-def test_eight_rank_routed_packed_sorted(gpu_device, inject):
+def test_eight_rank_routed_packed_sorted(gpu_device, monkeypatch, inject, combine):
     """The rehearsal of config 4's 8-GPU plan: 8 ranks on one GPU over the gloo communicator,
     16M records in 64 changesets (replica j whole on rank j % 8, records routed to key % 8).  The
     global frame fits, so records cross as 16-B packed wire records and every owner resolves them
     on the sorted path; a drift or a duplicate-node record raises at (41, 123,456).  Every row of all
-    8 shards, the canonical clock, status and exception fields against the C oracle."""
+    8 shards, the canonical clock, status and exception fields against the C oracle.  combine = 1:
+    each rank folds its home records to one packed maximum per key first (the map-side combine)."""
+    monkeypatch.setenv("CRDT_COMBINE", combine)
     kw = dict(seed=808, R=64, per_cs=250_000, n_local=1_500_000, n_new=600_000, millis_span=1 << 12,
               counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
     outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False, again=True)
     for rank, res, *_ in outs:
         assert res["path"] == "sorted" and res["plan"]["wire_packed"], (rank, res["plan"])
-        assert res["plan"]["own_in_place"], (rank, res["plan"])        # the second call on each ctx
+        assert res["plan"]["combined"] == (combine == "1"), (rank, res["plan"])
+        if combine == "0":
+            assert res["plan"]["own_in_place"], (rank, res["plan"])    # the second call on each ctx
         assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
         if inject:
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
