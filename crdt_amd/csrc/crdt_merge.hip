@@ -1529,6 +1529,8 @@ struct crdt_ctx {
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
+    DBuf<uint32_t> e_icnt;           // per emit item: entries, then [item][owner] entries
+    DBuf<uint64_t> e_off;            // [item][owner] offsets inside the owner's run
     bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
     DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
     DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
@@ -2070,7 +2072,7 @@ void prof_resolve_report() {
 // level-1 scatter and level 2 instead of before this function.
 int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
                  crdt_result* out, const PackFrame* anchor = nullptr, uint8_t* dflags = nullptr,
-                 const EmitOut* emit = nullptr) {
+                 EmitOut* emit = nullptr) {
     const uint32_t R = c->plan_R;
     // dflags (device, zeroed by the caller): the flagged form — packed records, stable level 2, the
     // ordered resolve with per-record flags, and the flags carried back to input order
@@ -2379,6 +2381,21 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
         if (em) {          // map-side combine: part folds, then every key's maximum emitted
+            // emit items: the resolve's max_items, then 16 carry blocks per hot bucket; kSKeys slots each
+            const uint32_t n_items = max_items + max_hot * (kSKeys / 256);
+            const size_t slots = (size_t)n_items * kSKeys;
+            HIPALLOC(c->e_key.ensure(slots));
+            HIPALLOC(c->e_pk.ensure(slots));
+            HIPALLOC(c->e_val.ensure(slots));
+            HIPALLOC(c->e_icnt.ensure((size_t)n_items * (1 + emit->G)));
+            HIPCHK(hipMemsetAsync(c->e_icnt.p, 0, (size_t)n_items * (1 + emit->G) * sizeof(uint32_t), c->stream));
+            emit->key = c->e_key.p;
+            emit->pk = c->e_pk.p;
+            emit->val = c->e_val.p;
+            emit->icount = c->e_icnt.p;
+            emit->ocount = c->e_icnt.p + n_items;
+            emit->item0 = max_items;
+            emit->n_items = n_items;
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
@@ -2808,6 +2825,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
+    c->e_icnt.release(); c->e_off.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
