@@ -1524,7 +1524,8 @@ struct crdt_ctx {
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     bool last_flagged = false;      // the last sorted apply was the flagged form
-    bool combine = true;            // sharded order-free merges fold home records before routing (CRDT_COMBINE=0: off)
+    int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
+                                    // 0 off, 1 auto = from 64 changesets, 2 always)
     bool last_combined = false;
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
@@ -2743,7 +2744,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_COMBINE")) c->combine = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;

@@ -410,10 +410,12 @@ def test_two_rank_packed_wire_gather_receiver(gpu_device, monkeypatch, name, kin
 @pytest.mark.parametrize("kind", ["routed", "parts"])
 @pytest.mark.parametrize("name", ["r4_ties", "r8_tombstones", "drift_late", "dup_node", "send_overflow",
                                   "explicit_millis"])
-def test_two_rank_combine(gpu_device, name, kind, world):
-    """The map-side combine (order-free, frame fits): each rank folds its home records into one
-    packed maximum per key (apply_sorted's emit mode), routes those, and the owners resolve them on
-    the sorted path — every shard row, canonical and exception fields vs the oracle."""
+def test_two_rank_combine(gpu_device, monkeypatch, name, kind, world):
+    """The map-side combine (order-free, frame fits; CRDT_COMBINE=2 forces it below 64 changesets):
+    each rank folds its home records into one packed maximum per key (apply_sorted's emit mode),
+    routes those, and the owners resolve them on the sorted path — every shard row, canonical and
+    exception fields vs the oracle."""
+    monkeypatch.setenv("CRDT_COMBINE", "2")
     outs = run_shard_gpu(dict(CASE_SPECS)[name], world, kind, path="auto", counts=False)
     for rank, res, *_ in outs:
         if res["status"] == 0 or res["plan"]["combined"]:
@@ -421,8 +423,8 @@ def test_two_rank_combine(gpu_device, name, kind, world):
 
 
 def test_two_rank_combine_hot_and_windows(gpu_device):
-    """Combine with split (hot) buckets on the home fold and on the owners: 240K records over 4096
-    keys in 120 changesets, ties and tombstones, 2 ranks."""
+    """Combine (auto: 120 changesets) with split (hot) buckets on the home fold and on the owners:
+    240K records over 4096 keys, ties and tombstones, 2 ranks."""
     kw = dict(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
               n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
     outs = run_shard_gpu(kw, 2, "routed", path="auto", counts=False)
@@ -534,7 +536,7 @@ def test_eight_rank_routed_packed_sorted(gpu_device, monkeypatch, inject, combin
     on the sorted path; a drift or a duplicate-node record raises at (41, 123,456).  Every row of all
     8 shards, the canonical clock, status and exception fields against the C oracle.  combine = 1:
     each rank folds its home records to one packed maximum per key first (the map-side combine)."""
-    monkeypatch.setenv("CRDT_COMBINE", combine)
+    monkeypatch.setenv("CRDT_COMBINE", combine)            # (64 changesets: auto combines)
     kw = dict(seed=808, R=64, per_cs=250_000, n_local=1_500_000, n_new=600_000, millis_span=1 << 12,
               counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
     outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False, again=True)
