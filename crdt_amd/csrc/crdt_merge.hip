@@ -1523,6 +1523,7 @@ struct crdt_ctx {
     bool flags_sorted = true;
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
+    int l2_items = 8;               // CRDT_L2_ITEMS=4: the packed level-2 scatter's 4-record sub-tiles (A/B)
     bool last_flagged = false;      // the last sorted apply was the flagged form
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
@@ -2347,8 +2348,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                     p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
             else if (pk)
                 if (k16)
-                    k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
+                    if (c->l2_items == 4)
+                        k_part_scatter2<false, true, true, true, true, 4><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0,
+                                                                           c->stream>>>(
+                            p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
+                    else
+                        k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                            p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
                 else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
@@ -2747,6 +2753,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
