@@ -1533,6 +1533,7 @@ struct crdt_ctx {
     DBuf<unsigned long long> e_cnt, e_cur;
     DBuf<uint32_t> e_icnt;           // per emit item: entries, then [item][owner] entries
     DBuf<uint64_t> e_off;            // [item][owner] offsets inside the owner's run
+    DBuf<unsigned long long> e_csum; // [chunk of 1024 items][owner] sums, then their offsets
     bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
     DBuf<uint16_t> f_pos1, f_pos2;  // run offsets: level 1 per input record, level 2 per level-1 record
     DBuf<uint8_t> f_flag1, f_flag2; // flags in level-1 / level-2 order
@@ -2833,7 +2834,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
-    c->e_icnt.release(); c->e_off.release();
+    c->e_icnt.release(); c->e_off.release(); c->e_csum.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
