@@ -285,7 +285,8 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         case, sel, part_offs = layout(_make_injected(case_kw), world, rank, kind)
         cap = -(-case["n_ids"] // world)
         t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
-        t.set_merge_path(path)
+        want_flags = path in ("gather", "sorted+flags")       # sorted+flags: the receivers' flagged form
+        t.set_merge_path("sorted" if path == "sorted+flags" else path)
         t.set_counts(counts)
         loc = case["local"]
         ids = np.arange(case["n_local"])
@@ -310,7 +311,7 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         dev = lambda a: None if a is None else torch.from_numpy(  # noqa: E731
             np.ascontiguousarray(a.view(np.int32) if a.dtype == np.uint32 else a)).cuda()
         millis = None if case["millis"] is None else dev(case["millis"][sel])
-        flags = torch.zeros(max(len(sel), 1), dtype=torch.uint8, device="cuda") if path == "gather" else False
+        flags = torch.zeros(max(len(sel), 1), dtype=torch.uint8, device="cuda") if want_flags else False
         cols = (dev(key.astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]), dev(case["val"][sel]))
         res, _ = t.merge(*cols, part_offs, case["wall"], millis=millis, win_flags=flags)
         if again:                 # the same call again on this ctx (receive columns sized by the first)
@@ -319,7 +320,7 @@ def _shard_gpu_worker(rank, world, port, case_kw, kind, q, backend="gloo", path=
         res["path"] = t.last_path()
         res["plan"] = t.last_plan()
         lt, rk, val, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
-        fl = flags[:len(sel)].cpu().numpy() if path == "gather" else None
+        fl = flags[:len(sel)].cpu().numpy() if want_flags else None
         q.put((rank, res, lt, rk, val, mod, sel, fl))
         t.close()
     finally:
@@ -357,7 +358,7 @@ def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True, a
         slots = keys[mine] // world
         for f, a in (("lt", lt), ("rank", rk), ("val", val), ("mod", mod)):
             assert np.array_equal(a[slots], orows[f][mine]), (kind, f)
-    if path == "gather":
+    if path in ("gather", "sorted+flags"):
         assert np.array_equal(flags, oflags)
     return outs
 
@@ -404,6 +405,17 @@ def test_two_rank_packed_wire_gather_receiver(gpu_device, monkeypatch, name, kin
     always resolve on the sorted path — test_two_rank_combine.)"""
     monkeypatch.setenv("CRDT_COMBINE", "0")
     run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path="auto", counts=False)
+
+
+@pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
+@pytest.mark.parametrize("name", ["r4_ties", "r8_tombstones", "drift_late", "dup_node", "explicit_millis"])
+def test_two_rank_flags_sorted_requested(gpu_device, name, kind):
+    """Win flags on a sharded ctx with the sorted path requested: the owners take K2 (the flagged form
+    runs on a single ctx), the flags travel back to the senders — every flag, shard row, canonical,
+    exception field and exact count vs the oracle."""
+    outs = run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path="sorted+flags", counts=True, again=True)
+    for rank, res, *_ in outs:
+        assert res["path"] == "gather" and not res["plan"]["flagged"], (rank, res["plan"])
 
 
 @pytest.mark.parametrize("world", [2, 3])
