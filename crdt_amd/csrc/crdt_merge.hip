@@ -2551,7 +2551,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
 bool use_sorted(const crdt_ctx* c, const Segs& sg, uint32_t R, const uint8_t* win_flags) {
     if (c->merge_path == 1 || c->canonical < 0 || c->cap > kSortedMaxCap) return false;
     // per-record win flags: the flagged form (packed records, one ctx; apply_segs checks the frame)
-    if (win_flags && (!c->flags_sorted || c->has_comm || !c->packed_resolve)) return false;
+    if (win_flags && (!c->flags_sorted || !c->packed_resolve)) return false;
     uint64_t n = 0, nw = 0;
     uint32_t jb = 0;
     for (size_t s = 0; s < sg.j.size(); ++s) {              // < 2^31 records per kWindow changesets

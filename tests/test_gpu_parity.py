@@ -409,13 +409,22 @@ def test_two_rank_packed_wire_gather_receiver(gpu_device, monkeypatch, name, kin
 
 @pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
 @pytest.mark.parametrize("name", ["r4_ties", "r8_tombstones", "drift_late", "dup_node", "explicit_millis"])
-def test_two_rank_flags_sorted_requested(gpu_device, name, kind):
-    """Win flags on a sharded ctx with the sorted path requested: the owners take K2 (the flagged form
-    runs on a single ctx), the flags travel back to the senders — every flag, shard row, canonical,
-    exception field and exact count vs the oracle."""
+def test_two_rank_flagged_receivers(gpu_device, name, kind):
+    """Win flags on a sharded ctx: the owners resolve their records on the sorted path's flagged form
+    (unpacked wire, the global frame; a changeset is one segment per source), the flags travel back
+    to the senders — every flag, shard row, canonical, exception field and exact count vs the oracle."""
     outs = run_shard_gpu(dict(CASE_SPECS)[name], 2, kind, path="sorted+flags", counts=True, again=True)
     for rank, res, *_ in outs:
-        assert res["path"] == "gather" and not res["plan"]["flagged"], (rank, res["plan"])
+        if res["path"] == "sorted":
+            assert res["plan"]["flagged"] and not res["plan"]["wire_packed"], (rank, res["plan"])
+
+
+def test_three_rank_flagged_receivers_fanin(gpu_device):
+    """A 300-changeset tie-heavy fan-in over 3 ranks with win flags on the receivers' flagged form."""
+    kw = dict(seed=79, R=300, per_cs=2000, n_local=40_000, n_new=20_000, millis_span=8, counter_span=4,
+              n_ranks=301)
+    outs = run_shard_gpu(kw, 3, "routed", path="sorted+flags", counts=True)
+    assert all(o[1]["plan"]["flagged"] for o in outs), [o[1]["plan"] for o in outs]
 
 
 @pytest.mark.parametrize("world", [2, 3])
