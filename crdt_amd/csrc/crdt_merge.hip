@@ -1523,6 +1523,7 @@ struct crdt_ctx {
     bool flags_sorted = true;
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
+    int fback_chk = 6;              // CRDT_FBACK_CHK = 0 / 4 / 6: the flag passes' run-search checkpoints (A/B)
     int l2_items = 8;               // CRDT_L2_ITEMS=4: the packed level-2 scatter's 4-record sub-tiles (A/B)
     bool last_flagged = false;      // the last sorted apply was the flagged form
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
@@ -2462,20 +2463,33 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint8_t* f1 = c->f_flag2.p;
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw));
-                if (k16)
-                    k_flags_back<false, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, kSBits - 4,
-                                                                          c->f_flag2.p, c->f_flag1.p, c->d_misc);
-                else
-                    k_flags_back<false, false><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, kSBits,
-                                                                           c->f_flag2.p, c->f_flag1.p, c->d_misc);
+#define CRDT_FBACK2(K16, SH, CHK)                                                                         \
+    k_flags_back<false, K16, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, SH, c->f_flag2.p, \
+                                                               c->f_flag1.p, c->d_misc)
+                if (k16) {
+                    if (c->fback_chk == 4) CRDT_FBACK2(true, kSBits - 4, 4);
+                    else if (c->fback_chk == 6) CRDT_FBACK2(true, kSBits - 4, 6);
+                    else CRDT_FBACK2(true, kSBits - 4, 0);
+                } else {
+                    if (c->fback_chk == 4) CRDT_FBACK2(false, kSBits, 4);
+                    else if (c->fback_chk == 6) CRDT_FBACK2(false, kSBits, 6);
+                    else CRDT_FBACK2(false, kSBits, 0);
+                }
+#undef CRDT_FBACK2
                 f1 = c->f_flag1.p;
                 // level 2 reused the tile -> segment index: rebuild level 1's
                 k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
                                                                                                  c->p_tseg.p);
             }
-            if (fl)
-            k_flags_back<true, false><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, cols.key,
-                                                                  shift1, f1, dflags, c->d_misc);
+#define CRDT_FBACK1(CHK)                                                                                  \
+    k_flags_back<true, false, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, cols.key, \
+                                                               shift1, f1, dflags, c->d_misc)
+            if (fl) {
+                if (c->fback_chk == 4) CRDT_FBACK1(4);
+                else if (c->fback_chk == 6) CRDT_FBACK1(6);
+                else CRDT_FBACK1(0);
+            }
+#undef CRDT_FBACK1
         } else if (c->counts) {
             k_resolve<true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec, rv,
                                                                     c->table, c->cap, c->d_Rj.p, jb, ps, cy, c->d_misc);
@@ -2755,6 +2769,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
+    if (const char* e = getenv("CRDT_FBACK_CHK")) c->fback_chk = atoi(e) == 4 ? 4 : atoi(e) == 0 ? 0 : 6;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);

@@ -1464,6 +1464,25 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
     assert res["path"] == "gather" and not res["plan"]["flagged"]
 
 
+@pytest.mark.parametrize("chk", ["0", "4"])
+def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk):
+    """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0) and with one per 16 staged
+    bytes (4; the default is one per 64): split hot bucket, cold buckets on the 2-B level-1 key
+    column, a late drift — same flags, rows and counts as the oracle."""
+    monkeypatch.setenv("CRDT_FBACK_CHK", chk)
+    case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
+                     n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
+    assert _flagged(case, _TWO)["plan"]["flagged"]
+    cold = _cold_bucket_case(95)
+    rows, res, flags = device_run(cold, path="sorted", flags=True, capacity=cold["n_ids"])
+    orows, ores, oflags = oracle_run(cold)
+    assert res["plan"]["flagged"] and res["plan"]["key16"] and np.array_equal(flags, oflags)
+    for f, a in zip(("lt", "rank", "val", "mod"), rows):
+        assert np.array_equal(a, orows[f]), f
+    res = _flagged(_late_drift_case(97), _TWO)
+    assert res["status"] == 1 and res["plan"]["flagged"]
+
+
 @pytest.mark.parametrize("K,total,R", [(1 << 20, 3_000_000, 64), (1 << 24, 9_000_000, 96)])
 def test_flagged_equals_gather_fanin(gpu_device, K, total, R):
     """A fan-in shape (Zipf keys, unique per replica, hot head split into parts) merged with flags on
