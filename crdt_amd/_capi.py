@@ -74,6 +74,7 @@ class CrdtCommOps(ctypes.Structure):
 
 
 COMM_ID_BYTES = 128
+ABI_VERSION = 3                            # include/crdt_merge.h CRDT_ABI_VERSION
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -149,6 +150,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.crdt_abi_version() != ABI_VERSION:      # struct layouts below are ABI_VERSION's
+        raise NativeLibraryMissing(f"{LIB_PATH} has ABI {lib.crdt_abi_version()}, the bindings ABI {ABI_VERSION}:"
+                                   " rebuild it")
     _lib = lib
     return lib
 

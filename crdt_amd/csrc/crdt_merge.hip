@@ -133,7 +133,9 @@ struct Misc {
     // k_bucket_items: the end of the last non-empty 4096-key bucket of the sorted path): the
     // table's high-water mark of written rows moves to it (crdt_ctx::hw)
     unsigned long long key_end;
-    unsigned long long route_own;   // k_route_plan: 1 = the own chunk is scattered into the receive columns
+    unsigned long long route_own;   // k_route_plan: bit 0 = the own chunk is scattered into the receive columns;
+                                    // bit 1 = the send counts do not add up to the batch (the scatters exit);
+                                    // bit 2 (k_shard_combine) = the ranks' collective-shape words differ
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
@@ -816,7 +818,8 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter(
 {
     PackFrame pf;
     const bool pk = route_frame(fm, frame_on, R, &pf);
-    if (!fm->route_own) own.slot = nullptr;
+    if (fm->route_own & 2) return;                   // a bad plan (k_route_plan): write nothing
+    if (!(fm->route_own & 1)) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
     const uint32_t j = jbase + blockIdx.y;
@@ -944,7 +947,8 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scatter_v(
 {
     PackFrame pf;
     const bool pk = route_frame(fm, frame_on, R, &pf);
-    if (!fm->route_own) own.slot = nullptr;
+    if (fm->route_own & 2) return;                   // a bad plan (k_route_plan): write nothing
+    if (!(fm->route_own & 1)) own.slot = nullptr;
     __shared__ uint32_t s_cnt[kRouteMaxRanks];
     __shared__ unsigned long long s_base[kRouteMaxRanks];
     const uint32_t j = jbase + blockIdx.y;
@@ -1039,8 +1043,8 @@ __global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt,
 __global__ __launch_bounds__(1024) void k_route_plan(const unsigned long long* __restrict__ cnt,
                                                      const unsigned long long* __restrict__ rcv, uint32_t G,
                                                      uint32_t R, uint32_t me, uint32_t own_in_recv,
-                                                     uint64_t recv_cap, unsigned long long* __restrict__ cursor,
-                                                     Misc* __restrict__ misc)
+                                                     uint64_t recv_cap, uint64_t n_send,
+                                                     unsigned long long* __restrict__ cursor, Misc* __restrict__ misc)
 {
     __shared__ unsigned long long s_wave[16];
     __shared__ unsigned long long s_carry, s_rd;
@@ -1078,8 +1082,11 @@ __global__ __launch_bounds__(1024) void k_route_plan(const unsigned long long* _
     block_scan(cnt, cells, cursor);                      // send positions, owner-major
     __threadfence_block();
     __syncthreads();
-    const bool own = own_in_recv && nr <= recv_cap;
-    if (tid == 0) misc->route_own = own ? 1ull : 0ull;
+    // the send columns hold n_send records: counts that do not add up to it (offsets and keys out of
+    // step) would send the scatter past them, so it writes nothing and the host fails the call
+    const bool bad = s_carry != n_send;
+    const bool own = own_in_recv && nr <= recv_cap && !bad;
+    if (tid == 0) misc->route_own = (own ? 1ull : 0ull) | (bad ? 2ull : 0ull);
     if (!own) return;
     const unsigned long long sd_me = cursor[(uint64_t)me * R];
     __syncthreads();
@@ -1097,9 +1104,12 @@ __global__ __launch_bounds__(256) void k_flags_back(const uint8_t* __restrict__ 
 
 // Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j, and
 // gsend[2R .. 2R + 4) = this rank's record frame (Misc::fr_*, max-accumulators).
-constexpr uint32_t kGatherExtra = 4;
+constexpr uint32_t kGatherExtra = 5;     // the frame's 4 words, then the rank's collective-shape word
+// gsend[2R + 4] = cfg: the per-process settings that shape the collectives after the clock phase
+// (comm_path.inc, shard_cfg_word); k_shard_combine checks that every rank sent the same one.
 __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict__ offs, uint32_t R,
-                                                     const Misc* __restrict__ misc, long long* __restrict__ gsend)
+                                                     const Misc* __restrict__ misc, long long* __restrict__ gsend,
+                                                     long long cfg)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j < R) gsend[R + j] = (long long)(offs[j + 1] - offs[j]);
@@ -1108,6 +1118,7 @@ __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict_
         gsend[2 * R + 1] = (long long)misc->fr_hi;
         gsend[2 * R + 2] = (long long)misc->fr_rlo;
         gsend[2 * R + 3] = (long long)misc->fr_rhi;
+        gsend[2 * R + 4] = cfg;
     }
 }
 
@@ -1129,6 +1140,9 @@ __global__ __launch_bounds__(256) void k_shard_combine(const long long* __restri
             a = w[0] > a ? w[0] : a; b = w[1] > b ? w[1] : b; c = w[2] > c ? w[2] : c; d = w[3] > d ? w[3] : d;
         }
         misc->fr_lo = a; misc->fr_hi = b; misc->fr_rlo = (uint32_t)c; misc->fr_rhi = (uint32_t)d;
+        bool same = true;                                   // every rank's collective-shape word alike
+        for (uint32_t r = 1; r < G; ++r) same = same && g[r * row + 2ull * R + 4] == g[2ull * R + 4];
+        if (!same) misc->route_own = 4ull;                  // (k_route_plan has not run yet)
     }
     if (j >= R) return;
     int64_t m = INT64_MIN, pm = INT64_MIN;
@@ -1532,7 +1546,8 @@ struct crdt_ctx {
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
-    DBuf<uint32_t> e_icnt;           // per emit item: entries, then [item][owner] entries
+    DBuf<uint32_t> e_icnt;           // per emit item: entries, first slots, then [item][owner] entries
+    DBuf<uint32_t> e_bbase;          // per bucket: its first emit slot (k_bucket_items)
     DBuf<uint64_t> e_off;            // [item][owner] offsets inside the owner's run
     DBuf<unsigned long long> e_csum; // [chunk of 1024 items][owner] sums, then their offsets
     bool last_ordered = false;      // ... or its ordered packed resolve (exact counts) without flags
@@ -2386,23 +2401,28 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
         if (ph) ev_record(c, ev_window(3, false));
-        k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc);
+        if (em) HIPALLOC(c->e_bbase.ensure(nb));
+        k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc,
+                                                                    em ? c->e_bbase.p : nullptr);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
         if (em) {          // map-side combine: part folds, then every key's maximum emitted
-            // emit items: the resolve's max_items, then 16 carry blocks per hot bucket; kSKeys slots each
+            // emit items: the resolve's max_items, then 16 carry blocks per hot bucket; the slots are the
+            // buckets' (k_bucket_items' ebase: min(kSKeys, records) each), so at most min(records, key range)
             const uint32_t n_items = max_items + max_hot * (kSKeys / 256);
-            const size_t slots = (size_t)n_items * kSKeys;
+            const size_t slots = (size_t)std::min<uint64_t>(nw, (uint64_t)nb * kSKeys) + 1;
             HIPALLOC(c->e_key.ensure(slots));
             HIPALLOC(c->e_pk.ensure(slots));
             HIPALLOC(c->e_val.ensure(slots));
-            HIPALLOC(c->e_icnt.ensure((size_t)n_items * (1 + emit->G)));
-            HIPCHK(hipMemsetAsync(c->e_icnt.p, 0, (size_t)n_items * (1 + emit->G) * sizeof(uint32_t), c->stream));
+            HIPALLOC(c->e_icnt.ensure((size_t)n_items * (2 + emit->G)));
+            HIPCHK(hipMemsetAsync(c->e_icnt.p, 0, (size_t)n_items * (2 + emit->G) * sizeof(uint32_t), c->stream));
             emit->key = c->e_key.p;
             emit->pk = c->e_pk.p;
             emit->val = c->e_val.p;
+            emit->bbase = c->e_bbase.p;
             emit->icount = c->e_icnt.p;
-            emit->ocount = c->e_icnt.p + n_items;
+            emit->ibase = c->e_icnt.p + n_items;
+            emit->ocount = c->e_icnt.p + 2 * (size_t)n_items;
             emit->item0 = max_items;
             emit->n_items = n_items;
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
@@ -2849,7 +2869,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
-    c->e_icnt.release(); c->e_off.release(); c->e_csum.release();
+    c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);

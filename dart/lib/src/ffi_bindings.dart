@@ -98,6 +98,10 @@ typedef _CtxOnlyC = Int32 Function(Pointer<Void>);
 typedef _CtxOnlyD = int Function(Pointer<Void>);
 
 const int crdtCommIdBytes = 128;
+/// include/crdt_merge.h CRDT_ABI_VERSION: the struct layouts above are this version's.
+const int crdtAbiVersion = 3;
+typedef _AbiC = Int32 Function();
+typedef _AbiD = int Function();
 
 /// The library's entry points, looked up once.
 class CrdtLib {
@@ -127,7 +131,15 @@ class CrdtLib {
         commFree = lib.lookupFunction<_CtxOnlyC, _CtxOnlyD>('crdt_comm_free'),
         setPresharded = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_presharded');
 
-  factory CrdtLib.open([String path = 'libcrdt_mi355x.so']) => CrdtLib(DynamicLibrary.open(path));
+  /// Opens the library and refuses one built against another ABI (crdt_timing / crdt_result layouts).
+  factory CrdtLib.open([String path = 'libcrdt_mi355x.so']) {
+    final lib = DynamicLibrary.open(path);
+    final abi = lib.lookupFunction<_AbiC, _AbiD>('crdt_abi_version')();
+    if (abi != crdtAbiVersion) {
+      throw StateError('$path has C-ABI $abi, these bindings expect $crdtAbiVersion');
+    }
+    return CrdtLib(lib);
+  }
 
   final _CreateD create;
   final _DestroyD destroy;

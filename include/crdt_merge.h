@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CRDT_ABI_VERSION 2
+#define CRDT_ABI_VERSION 3          /* 3: crdt_timing gained part1_records (round 3) */
 #define CRDT_NULL_VALUE 0xFFFFFFFFu
 
 /* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
@@ -245,8 +245,9 @@ int crdt_set_presharded(crdt_ctx* ctx, int presharded);
  * partitioned by key into 4096-key buckets, each bucket's rows are read and written
  * once and its records resolved in LDS; sorted_path.inc).  Both give identical
  * rows, canonical, status and counts.  The sorted path needs: canonical >= 0,
- * capacity <= 2^28; with win_flags, also a single ctx and a batch frame that fits its 64-bit
- * packed key (its flagged form), else the gather path runs.  path: CRDT_PATH_AUTO (default, also set by the
+ * capacity <= 2^28; with win_flags, also a batch frame that fits its 64-bit packed key (its
+ * flagged form; on a sharded ctx the receivers take it on the all-gathered global frame, with
+ * the records crossing the exchange unpacked), else the gather path runs.  path: CRDT_PATH_AUTO (default, also set by the
  * CRDT_MERGE_PATH environment variable = gather | sorted), CRDT_PATH_GATHER,
  * CRDT_PATH_SORTED (whenever allowed).  crdt_last_path reports the path the last
  * crdt_merge took (CRDT_PATH_GATHER or CRDT_PATH_SORTED). */

@@ -363,6 +363,67 @@ def run_shard_gpu(kw, world, kind, backend="gloo", path="gather", counts=True, a
     return outs
 
 
+def _mismatch_worker(rank, world, port, q, what):
+    """Two ranks whose collective-shape settings differ (win flags on one rank only, or counts): both
+    calls must fail with CRDT_E_INVALID before any exchange is posted (no hang, no corruption)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.device import CrdtNativeError
+    from crdt_amd.dist import GlooComm
+    from tests.test_dist_cpu import layout
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    _init_pg(dist, rank, world, "gloo")
+    try:
+        case, sel, part_offs = layout(make_case(**dict(CASE_SPECS)["r8_tombstones"]), world, rank, "routed")
+        cap = -(-case["n_ids"] // world)
+        t = DeviceTable(0, local_rank=case["local_rank"], capacity=cap)
+        t.comm_init_ops(world, rank, GlooComm(dist))
+        if what == "counts":
+            t.set_counts(rank == 0)
+        flags = what == "flags" and rank == 1
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a.view(np.int32) if a.dtype == np.uint32 else a)).cuda()  # noqa: E731
+        cols = (dev(case["key"][sel].astype(np.uint32)), dev(case["lt"][sel]), dev(case["rank"][sel]),
+                dev(case["val"][sel]))
+        c0 = t.canonical
+        before = t.read_rows(np.arange(cap, dtype=np.uint32))
+        try:
+            t.merge(*cols, part_offs, case["wall"], win_flags=flags)
+            st = 0
+        except CrdtNativeError as e:
+            st = e.status
+        after = t.read_rows(np.arange(cap, dtype=np.uint32))
+        q.put((rank, st, t.canonical == c0, all(np.array_equal(a, b) for a, b in zip(before, after))))
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("what", ["flags", "counts"])
+def test_two_rank_settings_mismatch_fails_fast(gpu_device, what):
+    """ADVICE r3 (comm_path.inc): the ranks' collective-shape words are all-gathered with the part maxima;
+    when they differ every rank returns CRDT_E_INVALID (nothing routed, canonical unchanged)."""
+    import torch.multiprocessing as mp
+
+    from tests.test_dist_cpu import _free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q, what)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=240) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, st, c_same, rows_same in outs:
+        assert st == -1, (rank, st)
+        assert c_same and rows_same, rank
+
+
 @pytest.mark.parametrize("kind", ["routed", "parts", "presharded"])
 @pytest.mark.parametrize("name", ["r8_tombstones", "dup_node", "drift_late", "send_overflow", "explicit_millis"])
 def test_two_rank_sharded_on_device(gpu_device, name, kind):
