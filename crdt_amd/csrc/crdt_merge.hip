@@ -224,12 +224,27 @@ __host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ul
 // straddling a changeset) into hist[ptb[j] + u][256] — what k_part_hist<true> would write with
 // every changeset applied (tiles of changesets >= stop are zeroed once stop is known).
 constexpr uint32_t kHistSub = 8;                 // scan tiles per level-1 partition tile
+
+// The level-1 digit of a key id.  One ctx: (k >> shift) & 255 over the ids k < cap.  The routed
+// partition of a sharded order-free merge (comm_path.inc, route_l1) partitions GLOBAL key ids of G = 2^gsh
+// ranks straight into their owners' level-1 buckets: owner o = k & (G - 1), slot k >> gsh (< cap, the
+// shard capacity), digit (o << dsh) | (slot >> shift) — every owner's 2^dsh digits, owner-major.  The
+// identity map {0, 8} is the one-ctx digit.
+struct KeyMap {
+    uint32_t gsh;
+    uint32_t dsh;
+};
+__host__ __device__ inline uint32_t km_digit(KeyMap m, uint32_t k, uint32_t shift) {
+    return ((((k & ((1u << m.gsh) - 1u)) << m.dsh) | ((k >> m.gsh) >> shift)) & 255u);
+}
+
 struct ScanHist {
     const uint32_t* key;
     const uint32_t* ptb;        // [R + 1] first partition tile of changeset j
     uint64_t cap;
     uint32_t shift;
     uint32_t* hist;
+    KeyMap km{0u, 8u};
 };
 
 // kVec: a thread's records are 4 groups of 4 consecutive ones (lt read with two 16-B loads per
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
 #pragma unroll
             for (int q = 0; q < kScanItems; ++q) {
                 const uint32_t k = kk[kHist ? q : 0];
-                digit_count(s_h, (k >> sh.shift) & 255u, k < sh.cap, lane);
+                digit_count(s_h, km_digit(sh.km, k, sh.shift), (k >> sh.km.gsh) < sh.cap, lane);
             }
         }
         // rank / millis matter only for records above C0 (the only ones recv() can raise on)
@@ -1543,6 +1558,13 @@ struct crdt_ctx {
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
     bool last_combined = false;
+    bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
+    bool last_route_l1 = false;     // the last sharded merge partitioned its home records into the owners' buckets
+    DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
+    DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
+    uint64_t rl_cap = 0;            // records both hold
+    DBuf<uint64_t> rl_plan;         // the owners' level-2 plan (segments, tiles, scan map)
+    HBuf<uint64_t> h_rlplan;
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
@@ -2237,12 +2259,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_part_scatter1<true, false, true, kL1Items, true, true, false, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p, hist1);
         else if (fl)
             k_part_scatter1<true, false, false, kL1Items, true, false, false, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p, hist1);
         else if (anchor && k16)
             k_part_scatter1<true, false, true, kL1AnchorItems, true, true, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
@@ -2353,13 +2375,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 const uint32_t jm = (uint32_t)pack_jmask(pf);
                 if (k16)
                     k_part_scatter2_seg<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        i12, p1k, tm2, kSBits - 4, t2p, o12, p2k, xper2, jm, pos2);
+                        i12, p1k, tm2, kSBits - 4, t2p, o12, p2k, xper2, jm, pos2, h2p);
                 else if (k8)
                     k_part_scatter2_seg<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2);
+                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2, h2p);
                 else
                     k_part_scatter2_seg<false, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2);
+                        i12, p1k, tm2, kSBits, t2p, o12, p2k, xper2, jm, pos2, h2p);
             } else if (c->counts)
                 k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
@@ -2483,18 +2505,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint8_t* f1 = c->f_flag2.p;
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw));
-#define CRDT_FBACK2(K16, SH, CHK)                                                                         \
-    k_flags_back<false, K16, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, p1k, SH, c->f_flag2.p, \
-                                                               c->f_flag1.p, c->d_misc)
-                if (k16) {
-                    if (c->fback_chk == 4) CRDT_FBACK2(true, kSBits - 4, 4);
-                    else if (c->fback_chk == 6) CRDT_FBACK2(true, kSBits - 4, 6);
-                    else CRDT_FBACK2(true, kSBits - 4, 0);
-                } else {
-                    if (c->fback_chk == 4) CRDT_FBACK2(false, kSBits, 4);
-                    else if (c->fback_chk == 6) CRDT_FBACK2(false, kSBits, 6);
-                    else CRDT_FBACK2(false, kSBits, 0);
-                }
+#define CRDT_FBACK2(CHK)                                                                                  \
+    k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, \
+                                                          c->d_misc)
+                if (c->fback_chk == 4) CRDT_FBACK2(4);
+                else if (c->fback_chk == 6) CRDT_FBACK2(6);
+                else CRDT_FBACK2(0);
 #undef CRDT_FBACK2
                 f1 = c->f_flag1.p;
                 // level 2 reused the tile -> segment index: rebuild level 1's
@@ -2502,8 +2518,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                                                  c->p_tseg.p);
             }
 #define CRDT_FBACK1(CHK)                                                                                  \
-    k_flags_back<true, false, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, cols.key, \
-                                                               shift1, f1, dflags, c->d_misc)
+    k_flags_back<true, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc)
             if (fl) {
                 if (c->fback_chk == 4) CRDT_FBACK1(4);
                 else if (c->fback_chk == 6) CRDT_FBACK1(6);
@@ -2786,6 +2801,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
+    if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
@@ -2870,6 +2886,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
     c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
+    c->rl_rec.release(); c->rl_k16.release(); c->rl_plan.release(); c->h_rlplan.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
@@ -3254,6 +3271,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_flagged) f |= CRDT_PLAN_FLAGGED;
         if (c->last_ordered) f |= CRDT_PLAN_ORDERED;
         if (c->last_combined) f |= CRDT_PLAN_COMBINED;
+        if (c->last_route_l1) f |= CRDT_PLAN_ROUTE_L1;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;

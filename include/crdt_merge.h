@@ -289,8 +289,11 @@ enum crdt_plan_flags {
     CRDT_PLAN_FLAGGED = 1024,    /* the sorted path's flagged form: per-record win flags (changeset-ordered
                                     level 2, ordered resolve, flags carried back to input order; sorted_path.inc) */
     CRDT_PLAN_ORDERED = 2048,    /* ... its ordered packed resolve (flags and / or exact n_present / n_won) */
-    CRDT_PLAN_COMBINED = 4096    /* sharded ctx: home records folded to one packed maximum per key before
+    CRDT_PLAN_COMBINED = 4096,   /* sharded ctx: home records folded to one packed maximum per key before
                                     the all-to-all (the order-free form's map-side combine) */
+    CRDT_PLAN_ROUTE_L1 = 8192    /* sharded ctx: home records partitioned once, straight into their owners'
+                                    level-1 buckets; 14-B level-1 records crossed the exchange and the
+                                    owners started at level 2 (comm_path.inc, route_l1) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

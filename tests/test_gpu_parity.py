@@ -552,19 +552,22 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R):
         t.comm_init_ops(world, rank, GlooComm(dist))
         res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
                          win_flags=False)
-        q.put((rank, res, t.last_path(), t.read_rows(np.arange(wl["capacity"], dtype=np.uint32))))
+        q.put((rank, res, t.last_path(), t.read_rows(np.arange(wl["capacity"], dtype=np.uint32)), t.last_plan()))
         t.close()
         torch.cuda.empty_cache()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("combine", ["1", "0"])
-def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine):
+@pytest.mark.parametrize("combine,route_l1", [("1", "1"), ("0", "1"), ("0", "0")])
+def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1):
     """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
     routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
-    map-side combine (each rank folds its home records per key before the exchange) and without."""
+    map-side combine (each rank folds its home records per key before the exchange), with the routed
+    level-1 partition (home records partitioned straight into the owners' level-1 buckets, owners from
+    level 2 on), and with plain record routing."""
     monkeypatch.setenv("CRDT_COMBINE", combine)
+    monkeypatch.setenv("CRDT_ROUTE_L1", route_l1)
     import torch.multiprocessing as mp
 
     from crdt_amd import DeviceTable
@@ -592,8 +595,10 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, res, path, shard in outs:
+    for rank, res, path, shard, plan in outs:
         assert path == "sorted"
+        assert plan["combined"] == (combine == "1"), plan
+        assert plan["route_l1"] == (combine == "0" and route_l1 == "1"), plan
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
             assert res[f] == ref[f], (rank, f)
         for a, b in zip(shard, rows):
@@ -627,6 +632,24 @@ def test_eight_rank_routed_packed_sorted(gpu_device, monkeypatch, inject, combin
         assert res["plan"]["combined"] == (combine == "1"), (rank, res["plan"])
         if combine == "0":
             assert res["plan"]["own_in_place"], (rank, res["plan"])    # the second call on each ctx
+        assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
+        if inject:
+            assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
+
+
+@pytest.mark.parametrize("inject", [None, "drift", "dup"])
+def test_eight_rank_route_l1(gpu_device, inject):
+    """The routed level-1 partition at G = 8 (comm_path.inc, route_l1): shards of > 2^20 slots (two
+    digits per owner), 16M records in 64 changesets, every rank partitioning its home records straight
+    into the 8 owners' level-1 buckets (14-B records over the exchange, own part in place), the owners
+    from level 2 on; a drift or duplicate-node record at (41, 123,456).  Every row of all 8 shards,
+    canonical, status and exception fields vs the C oracle, on two calls per ctx (buffers reused)."""
+    kw = dict(seed=818, R=64, per_cs=250_000, n_local=6_000_000, n_new=3_000_000, millis_span=1 << 12,
+              counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
+    outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False, again=True)
+    for rank, res, *_ in outs:
+        assert res["path"] == "sorted" and res["plan"]["route_l1"], (rank, res["plan"])
+        assert not res["plan"]["combined"], (rank, res["plan"])
         assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
         if inject:
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-4 GPU steps.  STAGE selects; every GPU step has its own time limit; stops at the first failure.
+#   flags : the flagged / ordered GPU tests, then the 1B flagged merge timing (tools/prof_flags.py)
+#   tests : the whole -m gpu suite (TESTS="-k expr" narrows it)
+#   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r4}
+case "${STAGE:-flags}" in
+  flags)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests \
+      -k "flagged or sorted or exact or ordered" > gpurun_out/${TAG}_pytest_flags.log 2>&1
+    rc=$?; tail -3 gpurun_out/${TAG}_pytest_flags.log; [ $rc -eq 0 ] || exit $rc
+    STEPS=${STEPS:-6} timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_time.log 2>&1
+    rc=$?; tail -8 gpurun_out/${TAG}_flags_time.log; exit $rc ;;
+  tests)
+    timeout -k 10 1100 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests ${TESTS:-} \
+      > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+    rc=$?; tail -3 gpurun_out/${TAG}_pytest_gpu.log; exit $rc ;;
+  ab)
+    STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
+    rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
+esac
