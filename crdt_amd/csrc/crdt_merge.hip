@@ -1558,6 +1558,7 @@ struct crdt_ctx {
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
     bool last_combined = false;
+    uint32_t sparse_t = 1024;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
     bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
     bool last_route_l1 = false;     // the last sharded merge partitioned its home records into the owners' buckets
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
@@ -2557,11 +2558,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             else if (k8)
                 k_resolve_packed<false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc);
+                    pf, c->d_misc, EmitOut{}, c->sparse_t);
             else
                 k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc);
+                    pf, c->d_misc, EmitOut{}, c->sparse_t);
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -2802,6 +2803,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;

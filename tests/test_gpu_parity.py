@@ -917,6 +917,21 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off, anchored
     assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
 
 
+@pytest.mark.parametrize("sparse_t", ["0", "1024", "1000000000"])
+@pytest.mark.parametrize("seed", [99, 5])
+def test_sorted_sparse_bucket_resolve(gpu_device, monkeypatch, sparse_t, seed):
+    """CRDT_SPARSE_T: buckets of fewer records than it fold their records from "absent" and read only
+    the touched keys' rows afterwards (0: every bucket loads its rows first; 10^9: every bucket below
+    the high-water mark is sparse) — the same rows, canonical and exception fields as the oracle, on
+    frame edges (rows below / at / above the frame, ranks outside it, exact ties) and on a case where a
+    part of the table lies above the high-water mark."""
+    monkeypatch.setenv("CRDT_SPARSE_T", sparse_t)
+    case = _frame_edge_case(seed) if seed == 99 else _cold_bucket_case(seed)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
+                              rank_bound=int(case["rank"].max()) + 1, device_cols=True)
+    assert res["plan"]["packed"] and res["plan"]["two_level"]
+
+
 def _cold_bucket_case(seed):
     """Keys spread over the whole of a > 2^20-key table: ~260 cold 4096-key buckets of a few
     hundred records each (no bucket near the 65,536-record split), so every resolve runs the

@@ -2,6 +2,8 @@
 # Round-4 GPU steps.  STAGE selects; every GPU step has its own time limit; stops at the first failure.
 #   flags : the flagged / ordered GPU tests, then the 1B flagged merge timing (tools/prof_flags.py)
 #   tests : the whole -m gpu suite (TESTS="-k expr" narrows it)
+#   shard : the multi-rank GPU tests (gloo ranks on one GPU, RCCL single rank)
+#   probe : one rank's local work at config 4's shares (tools/route_probe.py, PROBE_N="8 2")
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -19,6 +21,15 @@ case "${STAGE:-flags}" in
     timeout -k 10 1100 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests ${TESTS:-} \
       > gpurun_out/${TAG}_pytest_gpu.log 2>&1
     rc=$?; tail -3 gpurun_out/${TAG}_pytest_gpu.log; exit $rc ;;
+  shard)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
+      -k "rank or route or combine or shard or mismatch or rccl" > gpurun_out/${TAG}_pytest_shard.log 2>&1
+    rc=$?; tail -3 gpurun_out/${TAG}_pytest_shard.log; exit $rc ;;
+  probe)
+    for n in ${PROBE_N:-8 2}; do
+      N=$n STEPS=${STEPS:-3} timeout -k 10 400 python -u tools/route_probe.py > gpurun_out/${TAG}_probe_n$n.log 2>&1
+      rc=$?; grep -E "mean|rows|home" gpurun_out/${TAG}_probe_n$n.log; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_probe_n$n.log; exit $rc; }
+    done ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
