@@ -94,6 +94,8 @@ def main():
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        os.environ["CRDT_ENV_DYNAMIC"] = "1"         # route_ab below switches the routing per merge
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_rank %= max(torch.cuda.device_count(), 1)          # gloo rehearsal: several ranks per GPU
     torch.cuda.set_device(local_rank)
@@ -451,6 +453,34 @@ def main():
             parity = shard_parity(oracle, got, world) if oracle is not None else None
             del oracle
         barrier()
+    # ---- N > 1: one timed step in each way of moving the records (the same job; CRDT_ENV_DYNAMIC):
+    # route_l1 = home records partitioned straight into the owners' level-1 buckets (14-B level-1
+    # records over the exchange, owners from level 2 on), combine = the map-side fold first (16-B
+    # packed maxima), route = plain record routing (owners run the whole sorted path); DESIGN §7
+    route_ab = None
+    if world > 1 and args.config == "fanin":
+        route_ab = {"default_plan": {k: v for k, v in plan.items() if k in ("route_l1", "combined", "wire_packed")}}
+        modes = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1"},
+                 "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
+                 "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"}}
+        saved = {k: os.environ.get(k) for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1")}
+        for name, env in modes.items():
+            os.environ.update(env)
+            reset()
+            barrier()
+            ts = time.perf_counter()
+            r5 = step()
+            barrier()
+            ms5 = all_max(time.perf_counter() - ts) * 1e3
+            p5 = table.last_plan()
+            assert r5["status"] == 0 and r5["canonical_lt"] == res["canonical_lt"], (name, r5, res)
+            route_ab[name] = {"ms": round(ms5, 3), "value": round(total_records / (ms5 / 1e3), 1),
+                              "route_l1": p5["route_l1"], "combined": p5["combined"]}
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     # ---- pre-sharded figure (N > 1): every rank already holds exactly what it owns
     presharded = None
     if world > 1 and args.config == "fanin" and not args.no_presharded:
@@ -503,7 +533,7 @@ def main():
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
         "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
-        "pcie_inclusive": pcie, "presharded": presharded, "with_win_flags": with_flags,
+        "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "with_win_flags": with_flags,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),
                          "route": round(tsum.get("route_ms", 0) / K, 3),

@@ -1560,6 +1560,7 @@ struct crdt_ctx {
     bool last_combined = false;
     uint32_t sparse_t = 1024;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
     bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
+    bool rl1_split = true;          // CRDT_RL1_SPLIT=0: route_l1 partitions and sends in one piece
     bool last_route_l1 = false;     // the last sharded merge partitioned its home records into the owners' buckets
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
     DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
@@ -1594,6 +1595,8 @@ struct crdt_ctx {
     DBuf<unsigned long long> d_rcnt, d_rrecv;             // [G][R] route counts sent / received
     DBuf<unsigned long long> d_rcur;                      // [G][R] scatter cursors (k_route_plan)
     hipEvent_t route_ev = nullptr;                        // the route counts have reached the host
+    hipStream_t sstream = nullptr;                        // route_l1: the second half's partition
+    hipEvent_t rl_ev[2] = {nullptr, nullptr};             // route_l1: first half partitioned / second half
     uint64_t recv_cap = 0;                                // receive columns' capacity (records)
     HBuf<uint64_t> h_rcnt;                                // both, read back once per call
     DBuf<uint32_t> r_skey, r_srank, r_sval, r_key, r_rank, r_val;   // send / receive columns
@@ -2803,6 +2806,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_RL1_SPLIT")) c->rl1_split = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
@@ -2865,6 +2869,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
     c->d_rcur.release();
     if (c->route_ev) hipEventDestroy(c->route_ev);
+    for (hipEvent_t e : c->rl_ev) if (e) hipEventDestroy(e);
+    if (c->sstream) hipStreamDestroy(c->sstream);
     if (c->table.base) hipFree(c->table.base);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);

@@ -69,3 +69,6 @@ def test_bench_two_ranks_routed(gpu_device):
     assert d["value"] == pytest.approx(4000000 / (d["ms_per_step"] / 1e3), rel=1e-3)
     assert d["presharded"]["value"] > 0
     assert d["job"]["U_touch"] > 0 and d["job"]["U_win"] > 0
+    ab = d["route_ab"]                                          # one timed step per way of routing
+    assert ab["combine"]["combined"] and not ab["route"]["route_l1"] and not ab["route"]["combined"]
+    assert all(ab[m]["ms"] > 0 for m in ("route_l1", "combine", "route"))

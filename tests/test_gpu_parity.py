@@ -559,8 +559,8 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("combine,route_l1", [("1", "1"), ("0", "1"), ("0", "0")])
-def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1):
+@pytest.mark.parametrize("combine,route_l1,split", [("1", "1", "1"), ("0", "1", "1"), ("0", "1", "0"), ("0", "0", "1")])
+def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1, split):
     """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
     routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
     map-side combine (each rank folds its home records per key before the exchange), with the routed
@@ -568,6 +568,7 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
     level 2 on), and with plain record routing."""
     monkeypatch.setenv("CRDT_COMBINE", combine)
     monkeypatch.setenv("CRDT_ROUTE_L1", route_l1)
+    monkeypatch.setenv("CRDT_RL1_SPLIT", split)             # route_l1 in two pipelined pieces / in one
     import torch.multiprocessing as mp
 
     from crdt_amd import DeviceTable

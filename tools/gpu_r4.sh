@@ -4,6 +4,7 @@
 #   tests : the whole -m gpu suite (TESTS="-k expr" narrows it)
 #   shard : the multi-rank GPU tests (gloo ranks on one GPU, RCCL single rank)
 #   probe : one rank's local work at config 4's shares (tools/route_probe.py, PROBE_N="8 2")
+#   cfg3  : cfg3 with the sparse-bucket resolve on / off (in-process A/B), then its per-kernel PMC traffic
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -30,6 +31,12 @@ case "${STAGE:-flags}" in
       N=$n STEPS=${STEPS:-3} timeout -k 10 400 python -u tools/route_probe.py > gpurun_out/${TAG}_probe_n$n.log 2>&1
       rc=$?; grep -E "mean|rows|home" gpurun_out/${TAG}_probe_n$n.log; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_probe_n$n.log; exit $rc; }
     done ;;
+  cfg3)
+    timeout -k 10 500 python -u bench.py --config cfg3 --steps 8 --warmup 2 --no-cpu --no-pcie --ab CRDT_SPARSE_T=0,1024 \
+      > gpurun_out/${TAG}_cfg3_ab.json 2> gpurun_out/${TAG}_cfg3_ab.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_cfg3_ab.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_cfg3_ab.log; exit $rc; }
+    ARGS="--config cfg3 --steps 1 --warmup 0 --no-cpu --no-census --no-pcie" MERGES=1 PMC_OUT=${TAG}_pmc_cfg3.json \
+      bash tools/gpu_pmc_bench.sh ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
