@@ -1424,6 +1424,20 @@ struct HBuf {
 // Changeset segments of the columns an apply phase reads, in changeset order: segment s is
 // records [beg[s], end[s]) of changeset j[s].  One per changeset for a local batch; one per
 // (changeset, source rank) for records routed in by a sharded merge.
+// route_l1 (comm_path.inc): one piece's level-2 + resolve buffers at the owner (two pieces run at once)
+struct Rl1Scratch {
+    DBuf<uint32_t> hist, toff, part, choff, dstart2, tseg, ibase, ibucket, ksu32, kj2;
+    DBuf<int64_t> kslt;
+    DBuf<u32x4> rec2;
+    DBuf<uint64_t> plan;
+    HBuf<uint64_t> hplan;
+    void release() {
+        hist.release(); toff.release(); part.release(); choff.release(); dstart2.release(); tseg.release();
+        ibase.release(); ibucket.release(); ksu32.release(); kj2.release(); kslt.release(); rec2.release();
+        plan.release(); hplan.release();
+    }
+};
+
 struct Segs {
     std::vector<uint64_t> beg, end;
     std::vector<uint32_t> j;
@@ -1565,8 +1579,7 @@ struct crdt_ctx {
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
     DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
     uint64_t rl_cap = 0;            // records both hold
-    DBuf<uint64_t> rl_plan;         // the owners' level-2 plan (segments, tiles, scan map)
-    HBuf<uint64_t> h_rlplan;
+    Rl1Scratch rl_os[2];            // the owner's level 2 + resolve of each piece
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
@@ -1596,7 +1609,7 @@ struct crdt_ctx {
     DBuf<unsigned long long> d_rcur;                      // [G][R] scatter cursors (k_route_plan)
     hipEvent_t route_ev = nullptr;                        // the route counts have reached the host
     hipStream_t sstream = nullptr;                        // route_l1: the second half's partition
-    hipEvent_t rl_ev[2] = {nullptr, nullptr};             // route_l1: first half partitioned / second half
+    hipEvent_t rl_ev[4] = {};       // route_l1: piece 0 / 1 partitioned, piece 0 exchanged, piece 0 resolved
     uint64_t recv_cap = 0;                                // receive columns' capacity (records)
     HBuf<uint64_t> h_rcnt;                                // both, read back once per call
     DBuf<uint32_t> r_skey, r_srank, r_sval, r_key, r_rank, r_val;   // send / receive columns
@@ -2894,7 +2907,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
     c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
-    c->rl_rec.release(); c->rl_k16.release(); c->rl_plan.release(); c->h_rlplan.release();
+    c->rl_rec.release(); c->rl_k16.release(); c->rl_os[0].release(); c->rl_os[1].release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
