@@ -1565,11 +1565,14 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
 
 
 @pytest.mark.parametrize("chk", ["0", "4"])
-def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk):
+@pytest.mark.parametrize("bits", ["1", "0"])
+def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, bits):
     """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0) and with one per 16 staged
-    bytes (4; the default is one per 64): split hot bucket, cold buckets on the 2-B level-1 key
-    column, a late drift — same flags, rows and counts as the oracle."""
+    bytes (4; the default is one per 64), the flags between the passes as bits (CRDT_FLAG_BITS=1, the
+    default) or bytes: split hot bucket, cold buckets on the 2-B level-1 key column, a late drift —
+    same flags, rows and counts as the oracle."""
     monkeypatch.setenv("CRDT_FBACK_CHK", chk)
+    monkeypatch.setenv("CRDT_FLAG_BITS", bits)
     case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
                      n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
     assert _flagged(case, _TWO)["plan"]["flagged"]
