@@ -928,7 +928,8 @@ def test_sorted_sparse_bucket_resolve(gpu_device, monkeypatch, sparse_t, seed):
     part of the table lies above the high-water mark."""
     monkeypatch.setenv("CRDT_SPARSE_T", sparse_t)
     case = _frame_edge_case(seed) if seed == 99 else _cold_bucket_case(seed)
-    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False,
+                              capacity=(1 << 20) + 3 if seed == 99 else case["n_ids"],
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
 
