@@ -5,6 +5,7 @@
 #   shard : the multi-rank GPU tests (gloo ranks on one GPU, RCCL single rank)
 #   probe : one rank's local work at config 4's shares (tools/route_probe.py, PROBE_N="8 2")
 #   cfg3  : cfg3 with the sparse-bucket resolve on / off (in-process A/B), then its per-kernel PMC traffic
+#   fprof : kernel trace of the 1B flagged merge (tools/prof_flags.py)
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -13,8 +14,8 @@ export TMPDIR=/tmp
 TAG=${TAG:-r4}
 case "${STAGE:-flags}" in
   flags)
-    timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests \
-      -k "flagged or sorted or exact or ordered" > gpurun_out/${TAG}_pytest_flags.log 2>&1
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 170 --timeout-method thread -m gpu tests \
+      -k "(flagged or sorted or exact or ordered) and not rank" > gpurun_out/${TAG}_pytest_flags.log 2>&1
     rc=$?; tail -3 gpurun_out/${TAG}_pytest_flags.log; [ $rc -eq 0 ] || exit $rc
     STEPS=${STEPS:-6} timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_time.log 2>&1
     rc=$?; tail -8 gpurun_out/${TAG}_flags_time.log; exit $rc ;;
@@ -23,8 +24,8 @@ case "${STAGE:-flags}" in
       > gpurun_out/${TAG}_pytest_gpu.log 2>&1
     rc=$?; tail -3 gpurun_out/${TAG}_pytest_gpu.log; exit $rc ;;
   shard)
-    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
-      -k "rank or route or combine or shard or mismatch or rccl" > gpurun_out/${TAG}_pytest_shard.log 2>&1
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 170 --timeout-method thread -m gpu tests \
+      -k "${TESTS:-rank or route or combine or shard or mismatch or rccl}" > gpurun_out/${TAG}_pytest_shard.log 2>&1
     rc=$?; tail -3 gpurun_out/${TAG}_pytest_shard.log; exit $rc ;;
   probe)
     for n in ${PROBE_N:-8 2}; do
@@ -37,6 +38,14 @@ case "${STAGE:-flags}" in
     rc=$?; grep "A/B" gpurun_out/${TAG}_cfg3_ab.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_cfg3_ab.log; exit $rc; }
     ARGS="--config cfg3 --steps 1 --warmup 0 --no-cpu --no-census --no-pcie" MERGES=1 PMC_OUT=${TAG}_pmc_cfg3.json \
       bash tools/gpu_pmc_bench.sh ;;
+  fprof)
+    rm -rf gpurun_out/${TAG}_prof_flags
+    STEPS=${STEPS:-3} timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_flags -o run \
+      -- python3 tools/prof_flags.py > gpurun_out/${TAG}_prof_flags.log 2>&1
+    rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_flags.log; exit $rc; }
+    f=$(find gpurun_out/${TAG}_prof_flags -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$f" > gpurun_out/${TAG}_prof_flags_full.txt; grep step gpurun_out/${TAG}_prof_flags.log
+    head -24 gpurun_out/${TAG}_prof_flags_full.txt ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
