@@ -1565,7 +1565,7 @@ struct crdt_ctx {
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
-    bool flag_bits = true;          // CRDT_FLAG_BITS=0: the flagged form's level-2 / level-1 flags as bytes
+    int flag_bits = 1;              // CRDT_FLAG_BITS: 0 the flagged form's level-1 flags as bytes, 2 level 2's too
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     int fback_chk = 6;              // CRDT_FBACK_CHK = 0 / 4 / 6: the flag passes' run-search checkpoints (A/B)
     int l2_items = 8;               // CRDT_L2_ITEMS=4: the packed level-2 scatter's 4-record sub-tiles (A/B)
@@ -2492,11 +2492,14 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             HIPALLOC(c->f_cin_key.ensure(ksn));
             HIPALLOC(c->f_cin_val.ensure(ksn));
             HIPALLOC(c->f_cin_pres.ensure(ksn));
-            // flags between the passes as bits (CRDT_FLAG_BITS, two levels with flags; head32 keeps bytes)
-            const bool fbits = fl && two && c->flag_bits && !c->pf_head32;
+            // the flags in level-1 order as bits between the two flag passes (CRDT_FLAG_BITS=1, two levels;
+            // 2: the level-2 flags of the resolve too — measured slower: its extra registers cost the
+            // resolve its second workgroup per CU)
+            const bool fbits = fl && two && c->flag_bits != 0;
+            const bool fbits2 = fbits && c->flag_bits == 2 && !c->pf_head32;
             if (fl) HIPALLOC(c->f_flag2.ensure(nw + 8));
             uint8_t* fl2 = fl ? c->f_flag2.p : nullptr;
-            if (fbits) HIPCHK(hipMemsetAsync(fl2, 0, ((nw + 31) / 32) * 4, c->stream));
+            if (fbits2) HIPCHK(hipMemsetAsync(fl2, 0, ((nw + 31) / 32) * 4, c->stream));
             if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
@@ -2513,9 +2516,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     if (c->pf_head32) k_resolve_pflags<K8, T, true><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb,           \
         c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink, c->f_cin_val.p,        \
         c->f_cin_pres.p, pf, c->d_misc, fl2);                                                                   \
-    else if (fbits) k_resolve_pflags<K8, T, false, true><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb,     \
-        c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink, c->f_cin_val.p,        \
-        c->f_cin_pres.p, pf, c->d_misc, fl2);                                                                   \
+    else if (c->flag_bits == 2) k_resolve_pflags<K8, T, false, true><<<max_items, T, 0, c->stream>>>(bst,    \
+        d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,             \
+        c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);                                                   \
     else k_resolve_pflags<K8, T><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, \
                                                             c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,  \
                                                             c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2)
@@ -2530,8 +2533,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw + 8));
 #define CRDT_FBACK2(CHK)                                                                                  \
-    if (fbits) k_flags_back<false, CHK, true, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, \
+    if (fbits2) k_flags_back<false, CHK, true, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, \
                                                           c->f_flag2.p, c->f_flag1.p, c->d_misc);              \
+    else if (fbits) k_flags_back<false, CHK, false, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f,        \
+                                                          c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc); \
     else k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,      \
                                                           c->f_flag1.p, c->d_misc)
                 if (fbits) HIPCHK(hipMemsetAsync(c->f_flag1.p, 0, ((nw + 31) / 32) * 4, c->stream));
@@ -2836,7 +2841,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_FLAG_BITS")) c->flag_bits = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_FLAG_BITS")) c->flag_bits = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
     if (const char* e = getenv("CRDT_FBACK_CHK")) c->fback_chk = atoi(e) == 4 ? 4 : atoi(e) == 0 ? 0 : 6;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;

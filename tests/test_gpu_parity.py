@@ -1566,7 +1566,7 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
 
 
 @pytest.mark.parametrize("chk", ["0", "4"])
-@pytest.mark.parametrize("bits", ["1", "0"])
+@pytest.mark.parametrize("bits", ["1", "0", "2"])
 def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, bits):
     """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0) and with one per 16 staged
     bytes (4; the default is one per 64), the flags between the passes as bits (CRDT_FLAG_BITS=1, the
