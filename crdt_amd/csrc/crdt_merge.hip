@@ -1565,7 +1565,8 @@ struct crdt_ctx {
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
     int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
-    int flag_bits = 1;              // CRDT_FLAG_BITS: 0 the flagged form's level-1 flags as bytes, 2 level 2's too
+    int flag_bits = 0;              // CRDT_FLAG_BITS: 1 the flagged form's level-1 flags as bits, 2 level 2's too
+                                    // (measured slower, DESIGN §5.4: opt-in)
     bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     int fback_chk = 6;              // CRDT_FBACK_CHK = 0 / 4 / 6: the flag passes' run-search checkpoints (A/B)
     int l2_items = 8;               // CRDT_L2_ITEMS=4: the packed level-2 scatter's 4-record sub-tiles (A/B)
@@ -2492,9 +2493,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             HIPALLOC(c->f_cin_key.ensure(ksn));
             HIPALLOC(c->f_cin_val.ensure(ksn));
             HIPALLOC(c->f_cin_pres.ensure(ksn));
-            // the flags in level-1 order as bits between the two flag passes (CRDT_FLAG_BITS=1, two levels;
-            // 2: the level-2 flags of the resolve too — measured slower: its extra registers cost the
-            // resolve its second workgroup per CU)
+            // opt-in (CRDT_FLAG_BITS=1): the flags in level-1 order as bits between the two flag passes, two
+            // levels; 2: the level-2 flags of the resolve too.  Measured slower: the bit output of
+            // the first pass loads one 2-B position per lane, and the resolve's bit buffers spill registers
             const bool fbits = fl && two && c->flag_bits != 0;
             const bool fbits2 = fbits && c->flag_bits == 2 && !c->pf_head32;
             if (fl) HIPALLOC(c->f_flag2.ensure(nw + 8));
