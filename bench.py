@@ -44,6 +44,71 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+class GpuSampler:
+    """GPU clock / power / temperature sampled from the card's hwmon during the timed steps (no privileges
+    needed): freq1 = the graphics clock, freq2 = the memory clock, power1 = board power, temp2 / temp3.
+    Per step: mean / min / max of each, so a slow step or process can be matched with its clocks."""
+
+    FILES = {"sclk_mhz": ("freq1_input", 1e-6), "mclk_mhz": ("freq2_input", 1e-6), "power_w": ("power1_input", 1e-6),
+             "temp_edge_c": ("temp2_input", 1e-3), "temp_hot_c": ("temp3_input", 1e-3)}
+
+    def __init__(self, dev_index: int):
+        import glob
+        import threading
+        self.dir = None
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(dev_index)
+            slot = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            hw = glob.glob(f"/sys/bus/pci/devices/{slot}/hwmon/hwmon*")
+            self.dir, self.slot = (hw[0] if hw else None), slot
+        except Exception:  # noqa: BLE001 -- no sampler on this box
+            self.dir = None
+        self.samples, self.marks = [], []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        out = {}
+        for k, (f, sc) in self.FILES.items():
+            try:
+                with open(f"{self.dir}/{f}") as fh:
+                    out[k] = int(fh.read()) * sc
+            except (OSError, ValueError):
+                pass
+        return out
+
+    def _run(self):
+        while not self._stop.is_set():
+            self.samples.append((time.perf_counter(), self._read()))
+            time.sleep(0.002)
+
+    def start(self):
+        if self.dir:
+            self._t.start()
+        return self
+
+    def mark(self, t0: float, t1: float):
+        self.marks.append((t0, t1))
+
+    def stop(self) -> dict | None:
+        if not self.dir:
+            return None
+        self._stop.set()
+        self._t.join(timeout=2)
+        steps = []
+        for t0, t1 in self.marks:
+            win = [v for t, v in self.samples if t0 <= t <= t1]
+            st = {"samples": len(win)}
+            for k in self.FILES:
+                xs = [v[k] for v in win if k in v]
+                if xs:
+                    st[k] = [round(float(np.mean(xs)), 1), round(float(np.min(xs)), 1), round(float(np.max(xs)), 1)]
+            steps.append(st)
+        return {"source": f"{self.dir} (PCI {self.slot})", "per_step": steps,
+                "fields": "[mean, min, max] over the samples inside each timed step (~2 ms apart)"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -234,8 +299,9 @@ def main():
                                np.array([0, e - b], np.uint64)))
     table_timing = [False, []]                     # per-call timing records (streaming config)
     ab_ph = {}                                     # A/B: per-value phase timings of each step
+    step_phases = []                               # every timed step's phase timings
 
-    def timed_run(steps):
+    def timed_run(steps, sampler=None):
         step_ms, tsum, res = [], {}, None
         table.set_timing(True)
         table_timing[0] = True
@@ -247,7 +313,10 @@ def main():
             ts = time.perf_counter()
             res = step()
             barrier()
-            step_ms.append(all_max(time.perf_counter() - ts) * 1e3)       # max over ranks
+            te = time.perf_counter()
+            if sampler:
+                sampler.mark(ts, te)
+            step_ms.append(all_max(te - ts) * 1e3)       # max over ranks
             if ab:
                 ab[2].setdefault(ab[1][si % len(ab[1])], []).append(step_ms[-1])
             tms, table_timing[1] = table_timing[1] or [table.timing()], []
@@ -259,6 +328,7 @@ def main():
                 tm["apply_total"] = int(round(tm["apply_total"] * f))
             for k, v in tm.items():
                 tsum[k] = tsum.get(k, 0) + v
+            step_phases.append(tm)
             if ab:
                 ab_ph.setdefault(ab[1][si % len(ab[1])], []).append(tm)
         table.set_timing(False)
@@ -268,7 +338,25 @@ def main():
     for _ in range(args.warmup):
         reset()
         step()
-    step_ms, tsum, res = timed_run(args.steps)
+    sampler = GpuSampler(local_rank).start()
+    step_ms, tsum, res = timed_run(args.steps, sampler)
+    gpu_clocks = sampler.stop()
+    if gpu_clocks is not None and world == 1:       # this process's streaming copy rate (a 4 GiB device copy)
+        a = torch.empty(1 << 30, dtype=torch.int32, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a)
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(5):
+            b.copy_(a)
+        torch.cuda.synchronize()
+        gpu_clocks["copy_GBs"] = round(5 * 2 * a.numel() * 4 / (time.perf_counter() - ts) / 1e9, 1)
+        del a, b
+        torch.cuda.empty_cache()
+    if gpu_clocks:                                  # each step's time and level-1 scatter beside its clocks
+        for st, ms, ph in zip(gpu_clocks["per_step"], step_ms, step_phases):
+            st["step_ms"] = round(ms, 3)
+            st["part1_ms"] = round(ph.get("part1_ms", 0.0), 3)
     plan = table.last_plan()                        # (later merges — census, samples — may go elsewhere)
     if ab:
         for v, ms in ab[2].items():
@@ -534,6 +622,7 @@ def main():
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
         "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
         "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "with_win_flags": with_flags,
+        "gpu_clocks": gpu_clocks,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),
                          "route": round(tsum.get("route_ms", 0) / K, 3),

@@ -6,6 +6,9 @@
 #   probe : one rank's local work at config 4's shares (tools/route_probe.py, PROBE_N="8 2")
 #   cfg3  : cfg3 with the sparse-bucket resolve on / off (in-process A/B), then its per-kernel PMC traffic
 #   fprof : kernel trace of the 1B flagged merge (tools/prof_flags.py)
+#   bench : the default bench line + its PMC traffic + a kernel trace (profiles evidence)
+#   suite : the whole -m gpu suite, then smoke()
+#   spread: the short bench in REPS processes, clocks / power per step
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -46,6 +49,33 @@ case "${STAGE:-flags}" in
     f=$(find gpurun_out/${TAG}_prof_flags -name "*kernel_trace.csv" | head -1)
     python3 tools/ktrace_full.py "$f" > gpurun_out/${TAG}_prof_flags_full.txt; grep step gpurun_out/${TAG}_prof_flags.log
     head -24 gpurun_out/${TAG}_prof_flags_full.txt ;;
+  bench)
+    # the default bench line, its PMC traffic (two --pmc passes) and a kernel trace of the same command
+    timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
+    rc=$?; cat gpurun_out/${TAG}_bench_default.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_bench_default.log; exit $rc; }
+    PMC_OUT=${TAG}_pmc_bench.json bash tools/gpu_pmc_bench.sh || exit $?
+    rm -rf gpurun_out/${TAG}_prof_bench
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_bench -o run \
+      -- python3 bench.py --no-cpu > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof_bench.log
+    rc=$?; echo "[prof] exit $rc"; [ $rc -eq 0 ] || exit $rc
+    t=$(find gpurun_out/${TAG}_prof_bench -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$t" > gpurun_out/${TAG}_prof_bench_full.txt; head -16 gpurun_out/${TAG}_prof_bench_full.txt ;;
+  suite)
+    timeout -k 10 1000 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests \
+      > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+    rc=$?; tail -3 gpurun_out/${TAG}_pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1
+    rc=$?; tail -2 gpurun_out/${TAG}_smoke.log; exit $rc ;;
+  spread)
+    # process-to-process spread: the same short bench in REPS processes, each line with its per-step clocks
+    for i in $(seq 1 ${REPS:-3}); do
+      timeout -k 10 300 python -u bench.py --steps 6 --warmup 2 --no-cpu --no-census --no-pcie \
+        > gpurun_out/${TAG}_spread_$i.json 2> gpurun_out/${TAG}_spread_$i.log
+      rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_spread_$i.log; exit $rc; }
+      python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_spread_$i.json')); g=d.get('gpu_clocks') or {}
+print('run $i', d['ms_per_step'], 'copy', g.get('copy_GBs'), [(s.get('step_ms'), s.get('part1_ms'), s.get('sclk_mhz'), s.get('power_w')) for s in g.get('per_step', [])])"
+    done ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
