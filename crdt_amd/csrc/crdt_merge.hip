@@ -1386,16 +1386,26 @@ static bool poison_alloc() {
     static const int v = [] { const char* e = getenv("CRDT_POISON_ALLOC"); return e && atoi(e) ? 1 : 0; }();
     return v != 0;
 }
+// CRDT_ALLOC_CONTIG=1: the partition buffers (the level-1 / level-2 scatters' scattered destinations) are
+// allocated physically contiguous (hipDeviceMallocContiguous; plain hipMalloc if that fails) — the
+// placement experiment of DESIGN §6 (the level-1 scatter's process-to-process spread).
+static bool contig_alloc() {
+    static const int v = [] { const char* e = getenv("CRDT_ALLOC_CONTIG"); return e && atoi(e) ? 1 : 0; }();
+    return v != 0;
+}
 
 template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
-    hipError_t ensure(size_t want) {
+    hipError_t ensure(size_t want, bool contig = false) {
         if (want <= n && p) return hipSuccess;
         if (p) { hipFree(p); p = nullptr; n = 0; }
         size_t m = std::max<size_t>(want, 16);
-        hipError_t e = hipMalloc(&p, m * sizeof(T));
+        hipError_t e = hipErrorMemoryAllocation;
+        if (contig && contig_alloc())
+            e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p), m * sizeof(T), hipDeviceMallocContiguous);
+        if (e != hipSuccess) e = hipMalloc(&p, m * sizeof(T));
         if (e == hipSuccess) n = m;
         if (e == hipSuccess && poison_alloc()) {      // (finished before any stream's next use)
             e = hipMemset(p, 0x5A, m * sizeof(T));
@@ -2237,7 +2247,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
         // partition buffers, each base shifted by the CRDT_L{1,2}_SHIFT knob (KB; placement A/B runs)
         constexpr size_t kShiftPad = 4u << 20;                      // bytes
-        HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4));
+        HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4, true));
         u32x4* p1r = c->p1_rec.p + (size_t)c->l1_shift_kb * 64;
         uint32_t* p1k = c->p1_kj.p + (size_t)c->l1_shift_kb * 256;
         u32x4* p2r = nullptr;
@@ -2343,7 +2353,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
-            HIPALLOC(c->p2_rec.ensure(nw + kShiftPad / 16)); HIPALLOC(c->p2_kj.ensure(nw + kShiftPad / 4));
+            HIPALLOC(c->p2_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p2_kj.ensure(nw + kShiftPad / 4, true));
             p2r = c->p2_rec.p + (size_t)c->l2_shift_kb * 64;
             p2k = c->p2_kj.p + (size_t)c->l2_shift_kb * 256;
             uint32_t* tb2 = c->p_l2map.p;
@@ -2976,10 +2986,10 @@ int crdt_reserve_scratch(crdt_ctx* c, uint64_t n_records) {
     if (n_records == 0) return CRDT_OK;
     HIPCHK(hipSetDevice(c->device));
     constexpr size_t kShiftPad = 4u << 20;        // as apply_sorted sizes them
-    HIPALLOC(c->p1_rec.ensure(n_records + kShiftPad / 16));
-    HIPALLOC(c->p1_kj.ensure(n_records + kShiftPad / 4));
-    HIPALLOC(c->p2_rec.ensure(n_records + kShiftPad / 16));
-    HIPALLOC(c->p2_kj.ensure(n_records + kShiftPad / 4));
+    HIPALLOC(c->p1_rec.ensure(n_records + kShiftPad / 16, true));
+    HIPALLOC(c->p1_kj.ensure(n_records + kShiftPad / 4, true));
+    HIPALLOC(c->p2_rec.ensure(n_records + kShiftPad / 16, true));
+    HIPALLOC(c->p2_kj.ensure(n_records + kShiftPad / 4, true));
     return CRDT_OK;
 }
 
