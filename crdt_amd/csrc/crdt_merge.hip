@@ -1595,6 +1595,7 @@ struct crdt_ctx {
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
+    HBuf<unsigned long long> h_ebase;   // the combine's owner bases (pinned staging of e_cur)
     DBuf<uint32_t> e_icnt;           // per emit item: entries, first slots, then [item][owner] entries
     DBuf<uint32_t> e_bbase;          // per bucket: its first emit slot (k_bucket_items)
     DBuf<uint64_t> e_off;            // [item][owner] offsets inside the owner's run
@@ -2937,6 +2938,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->f_hist2.release(); c->f_toff2.release();
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
     c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
+    c->h_ebase.release();
     c->rl_rec.release(); c->rl_k16.release(); c->rl_os[0].release(); c->rl_os[1].release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
