@@ -5,12 +5,13 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-rm -rf gpurun_out/pmc_flags_sq
-MIX=1 STEPS=4 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_flags_sq -o run -- python3 tools/prof_flags.py > gpurun_out/pmc_flags_sq.log 2>&1
-rc=$?; echo "[pmc] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_flags_sq.log; exit $rc; }
-python3 - <<'PY'
-import csv, glob, collections
-f = glob.glob("gpurun_out/pmc_flags_sq/**/*counter_collection.csv", recursive=True)[0]
+OUT=${OUT:-pmc_flags_sq}
+rm -rf gpurun_out/$OUT
+MIX=1 STEPS=4 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d gpurun_out/$OUT -o run -- python3 tools/prof_flags.py > gpurun_out/$OUT.log 2>&1
+rc=$?; echo "[pmc] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/$OUT.log; exit $rc; }
+OUT=$OUT python3 - <<'PY'
+import csv, glob, collections, os
+f = glob.glob(f"gpurun_out/{os.environ['OUT']}/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
 for r in csv.DictReader(open(f)):
     k = r["Kernel_Name"]

@@ -9,6 +9,7 @@
 #   bench : the default bench line + its PMC traffic + a kernel trace (profiles evidence)
 #   suite : the whole -m gpu suite, then smoke()
 #   spread: the short bench in REPS processes, clocks / power per step
+#   misc  : wide-frame fan-in with flags, anchored-form PMC, flagged-form SQ counters
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -77,6 +78,17 @@ case "${STAGE:-flags}" in
 import json; d=json.load(open('gpurun_out/${TAG}_spread_$i.json')); g=d.get('gpu_clocks') or {}
 print('run $i contig=${CRDT_ALLOC_CONTIG:-0}', d['ms_per_step'], 'part1', d['roofline']['dominant_kernel']['phases_ms_per_step']['part1'], 'copy', g.get('copy_GBs'), [(s.get('step_ms'), s.get('part1_ms'), s.get('sclk_mhz'), s.get('power_w')) for s in g.get('per_step', [])])"
     done ;;
+  misc)
+    # the wide clock frame with win flags; the anchored form's PMC traffic (item 3);
+    # SQ counters of the flagged form's kernels (item 2)
+    timeout -k 10 600 python -u bench.py --millis-span 67108864 --steps 3 --warmup 1 --no-pcie --no-cpu-copy16 \
+      --cpu-seconds 5 > gpurun_out/${TAG}_bench_wide26.json 2> gpurun_out/${TAG}_bench_wide26.log
+    rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_bench_wide26.log; exit $rc; }
+    python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_bench_wide26.json')); w=d['with_win_flags']
+print('wide26', d['ms_per_step'], d['roofline']['dominant_kernel']['plan'].get('key16'), 'flags', w['ms_per_step'], w['merge_path'], w['flagged_form'], w.get('flags_equal_gather'), 'parity', (d['parity'] or {}).get('equal'))"
+    CRDT_SORTED_FORM=262144 PMC_OUT=${TAG}_pmc_anchored.json bash tools/gpu_pmc_bench.sh || exit $?
+    OUT=${TAG}_pmc_flags_sq bash tools/gpu_pmc_flags.sh ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
