@@ -1781,8 +1781,10 @@ inline void ev_record(crdt_ctx* c, size_t idx) {
 // the scan then reads every rank with its lt).
 // bound_ok: the frame's rank part may come from crdt_set_rank_bound (single ctx; a sharded merge
 // reduces the ranks' own frame, which the packed wire records are encoded against).
+// route_km (a sharded merge that will likely partition its home records into the owners' level-1 buckets,
+// comm_path.inc route_l1): the scan also counts the routed level-1 histogram (keys read with lt and rank).
 int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_maxima, bool allow_fuse = false,
-               bool frame = false, bool bound_ok = true, bool keys_ready = false) {
+               bool frame = false, bool bound_ok = true, bool keys_ready = false, const KeyMap* route_km = nullptr) {
     c->fused = false;
     c->resolved = false;
     c->hist1_fused = false;
@@ -1815,12 +1817,16 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     // (a host batch arrives here as device columns whose keys are still being copied: keys_ready)
     const bool hist = c->frame_lt_only && c->hist_fuse && keys_ready && home->mem == CRDT_MEM_DEVICE &&
                       R <= kWindow && tiles > 0 && home->key_id;
-    if (hist) {
+    const bool rhist = !hist && route_km && frame && c->hist_fuse && R <= kWindow && tiles > 0 && home->key_id &&
+                       !home->millis;
+    if (hist || rhist) {
         HIPALLOC(c->p_hist1.ensure(c->plan_ptiles * kDigits));
         c->hist1_fused = true;
         c->hist1_key = home->key_id;
-        c->hist1_shift = c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
+        c->hist1_shift = rhist || c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
     }
+    ScanHist shr{home->key_id, c->d_ptb, c->cap, 20u, c->p_hist1.p};
+    if (rhist) shr.km = *route_km;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
         const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
@@ -1828,7 +1834,11 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t gxh = std::max<uint32_t>(1, std::min<uint32_t>((mt + kHistSub - 1) / kHistSub, cap_x));
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
-            if (hist && !(c->form_off & kFormNoVecScan))
+            if (rhist)                                    // routed histogram: rank read with lt (the frame)
+                k_scan<true, false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                    cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shr);
+            else if (hist && !(c->form_off & kFormNoVecScan))
                 k_scan<false, true, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
