@@ -335,6 +335,17 @@ def main():
         table_timing[0] = False
         return step_ms, tsum, res
 
+    # N > 1 fan-in: the library's routing tuner (comm_path.inc RouteTune) takes its trial calls — each way of
+    # moving the records twice, the faster kept — before the warmup, so every timed step takes the chosen way
+    route_tune = None
+    if world > 1 and args.config == "fanin" and os.environ.get("CRDT_ROUTE_TUNE", "1") != "0":
+        for _ in range(6):
+            reset()
+            step()
+            if table.route_tune()["best"] is not None:
+                break
+        route_tune = table.route_tune()
+        log(f"routing tuner: {route_tune}")
     for _ in range(args.warmup):
         reset()
         step()
@@ -621,7 +632,7 @@ def main():
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
         "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
-        "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "with_win_flags": with_flags,
+        "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "route_tune": route_tune, "with_win_flags": with_flags,
         "gpu_clocks": gpu_clocks,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),

@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <vector>
 
@@ -1588,6 +1589,20 @@ struct crdt_ctx {
     bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
     bool rl1_split = true;          // CRDT_RL1_SPLIT=0: route_l1 partitions and sends in one piece
     bool last_route_l1 = false;     // the last sharded merge partitioned its home records into the owners' buckets
+    // the routing of a sharded order-free fan-in, measured (comm_path.inc, RouteTune): route_l1 sends 14-B
+    // partition records, the combine folds first and sends ~3.4x fewer bytes at more local work; which is
+    // faster depends on the links, so the ctx times each (two calls each, max over ranks) and keeps the faster
+    bool route_tune = true;         // CRDT_ROUTE_TUNE=0: the fixed rule (combine at G = 2, route_l1 from G = 4)
+    struct RouteTune {
+        uint64_t shape = 0;         // (R, G, cap) the trials were taken for
+        uint32_t trial = 0;         // trial calls taken (kTrials per way)
+        int best = -1;              // 0 route_l1, 1 combine; -1 while trials run
+        long long us[2] = {-1, -1}; // each way's second call, max over ranks (microseconds)
+    } rt;
+    int tune_mode = -1;             // this call's way from the tuner (-1: the fixed rule)
+    bool tune_trial = false;        // ... and the call took it with both ways open (a trial / a tuned call)
+    DBuf<long long> d_tune;         // the trial time's MAX all-reduce word
+    HBuf<long long> h_tune;         // ... its pinned staging
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
     DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
     uint64_t rl_cap = 0;            // records both hold
@@ -2860,6 +2875,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
     if (const char* e = getenv("CRDT_RL1_SPLIT")) c->rl1_split = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_ROUTE_TUNE")) c->route_tune = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
     if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
@@ -2919,7 +2935,7 @@ void crdt_destroy(crdt_ctx* c) {
     comm_release(c);
     for (auto* b : {&c->r_skey, &c->r_srank, &c->r_sval, &c->r_key, &c->r_rank, &c->r_val}) b->release();
     c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
-    c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release();
+    c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release(); c->d_tune.release(); c->h_tune.release();
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
     c->d_rcur.release();
     if (c->route_ev) hipEventDestroy(c->route_ev);
@@ -3338,7 +3354,16 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;
+    if (c->tune_trial) f |= CRDT_PLAN_ROUTE_TUNED;
     *flags = f;
+    return CRDT_OK;
+}
+
+int crdt_route_tune_info(const crdt_ctx* c, int32_t* best, int64_t* us) {
+    if (!c || !best || !us) return CRDT_E_INVALID;
+    *best = c->rt.best;
+    us[0] = c->rt.us[0];
+    us[1] = c->rt.us[1];
     return CRDT_OK;
 }
 

@@ -312,13 +312,23 @@ class DeviceTable:
     PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32,
                   "high_water": 64, "anchored": 128, "wire_packed": 256, "own_in_place": 512,
                   "flagged": 1024, "ordered": 2048,
-                  "combined": 4096, "route_l1": 8192}
+                  "combined": 4096, "route_l1": 8192, "route_tuned": 16384}
 
     def last_plan(self) -> dict:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""
         v = ctypes.c_uint32(0)
         self._check(self._lib.crdt_last_plan(self._ctx, ctypes.byref(v)), "crdt_last_plan")
         return {k: bool(v.value & b) for k, b in self.PLAN_FLAGS.items()}
+
+    def route_tune(self) -> dict:
+        """crdt_route_tune_info: the sharded fan-in routing the ctx measured ({'best': None while the
+        trials run, else 'route_l1' / 'combine'; 'route_l1_ms' / 'combine_ms': each way's timed call,
+        max over ranks, None if not yet})."""
+        best = ctypes.c_int32(0)
+        us = (ctypes.c_int64 * 2)()
+        self._check(self._lib.crdt_route_tune_info(self._ctx, ctypes.byref(best), us), "crdt_route_tune_info")
+        ms = [u / 1e3 if u >= 0 else None for u in us]
+        return {"best": {0: "route_l1", 1: "combine"}.get(best.value), "route_l1_ms": ms[0], "combine_ms": ms[1]}
 
     def set_timing(self, enable: bool):
         self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")

@@ -20,3 +20,10 @@ def gpu_device():
     n = _capi.device_count()
     assert n > 0, "no gfx950 device visible: GPU tests need an MI355X"
     return 0
+
+
+@pytest.fixture(autouse=True)
+def _fixed_routing(monkeypatch):
+    """Sharded fan-ins take the fixed routing rule in tests (each way is asserted explicitly); the routing
+    tuner, which picks a way per ctx from measured calls, has its own test (test_two_rank_route_tune)."""
+    monkeypatch.setenv("CRDT_ROUTE_TUNE", "0")

@@ -54,10 +54,10 @@ def test_bench_two_ranks_routed(gpu_device):
     """The N > 1 bench path (config 4: the same records in total, replica j on rank j % N, routed
     to key % N inside the library's collective merge) with 2 ranks on one GPU over the gloo
     communicator: the driver's N = 2..8 runs take the same code with RCCL, one GPU per rank."""
-    env = dict(os.environ, CRDT_BENCH_BACKEND="gloo")
+    env = dict(os.environ, CRDT_BENCH_BACKEND="gloo", CRDT_ROUTE_TUNE="1")   # (64 changesets: the tuner runs)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--records", "4000000", "--replicas", "16"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--records", "4000000", "--replicas", "64"]
     # (default key space: torch.distributed.run's own parser takes `--local` for `--local-addr`)
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -72,3 +72,6 @@ def test_bench_two_ranks_routed(gpu_device):
     ab = d["route_ab"]                                          # one timed step per way of routing
     assert ab["combine"]["combined"] and not ab["route"]["route_l1"] and not ab["route"]["combined"]
     assert all(ab[m]["ms"] > 0 for m in ("route_l1", "combine", "route"))
+    tune = d["route_tune"]                                      # the way every timed step took, measured
+    assert tune["best"] in ("route_l1", "combine") and tune["route_l1_ms"] > 0 and tune["combine_ms"] > 0
+    assert ab["default_plan"]["combined"] == (tune["best"] == "combine")

@@ -528,8 +528,9 @@ def test_rccl_single_rank_sorted(gpu_device):
     assert outs[0][1]["path"] == "sorted"
 
 
-def _fanin_shard_worker(rank, world, port, q, K, total, R):
-    """Routed fan-in (gen_fanin's home layout) on one rank; returns this shard's rows."""
+def _fanin_shard_worker(rank, world, port, q, K, total, R, calls=1):
+    """Routed fan-in (gen_fanin's home layout) on one rank, `calls` times from the same table; returns this
+    shard's rows after each call (with the call's result, path and plan) and the ctx's routing tuner."""
     import os
 
     import torch
@@ -547,12 +548,19 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R):
         t.set_counts(False)
         t.set_merge_path("sorted")
         loc, home = wl["local"], wl["home"]
-        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
-        t.canonical = wl["c0"]
         t.comm_init_ops(world, rank, GlooComm(dist))
-        res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
-                         win_flags=False)
-        q.put((rank, res, t.last_path(), t.read_rows(np.arange(wl["capacity"], dtype=np.uint32)), t.last_plan()))
+        got = []
+        for _ in range(calls):
+            t.clear_rows(0, wl["capacity"])
+            t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+            t.canonical = wl["c0"]
+            res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
+                             win_flags=False)
+            got.append((res, t.last_path(), t.read_rows(np.arange(wl["capacity"], dtype=np.uint32)), t.last_plan()))
+        if calls == 1:
+            q.put((rank,) + got[0])
+        else:
+            q.put((rank, got, t.route_tune()))
         t.close()
         torch.cuda.empty_cache()
     finally:
@@ -569,6 +577,7 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
     monkeypatch.setenv("CRDT_COMBINE", combine)
     monkeypatch.setenv("CRDT_ROUTE_L1", route_l1)
     monkeypatch.setenv("CRDT_RL1_SPLIT", split)             # route_l1 in two pipelined pieces / in one
+    monkeypatch.setenv("CRDT_ROUTE_TUNE", "0")               # the fixed rule (the tuner: the test below)
     import torch.multiprocessing as mp
 
     from crdt_amd import DeviceTable
@@ -604,6 +613,61 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
             assert res[f] == ref[f], (rank, f)
         for a, b in zip(shard, rows):
             assert np.array_equal(a, b[rank::2]), rank
+
+
+def _fanin_reference(K, total, R):
+    """The unsharded K2 merge of gen_fanin's whole job: (result, all rows)."""
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+    t.set_merge_path("gather")
+    loc, own = wl["local"], wl["owned"]
+    t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+    t.canonical = wl["c0"]
+    ref, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                     win_flags=False)
+    rows = t.read_rows(np.arange(K, dtype=np.uint32))
+    t.close()
+    return ref, rows
+
+
+def test_two_rank_route_tune(gpu_device, monkeypatch):
+    """The routing tuner (comm_path.inc RouteTune, the auto settings): the first calls take route_l1 twice
+    and the map-side combine twice, every later call the way whose timed call was faster (max over the
+    ranks, the same way on both ranks); every call leaves exactly the unsharded merge's rows."""
+    for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_ROUTE_TUNE", "CRDT_RL1_SPLIT"):
+        monkeypatch.delenv(k, raising=False)
+    import torch.multiprocessing as mp
+
+    from tests.test_dist_cpu import _free_port
+    K, total, R = 1 << 22, 4_000_000, 128
+    ref, rows = _fanin_reference(K, total, R)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 6)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tunes = [o[2] for o in outs]
+    assert tunes[0] == tunes[1], tunes                        # one decision, from the max over ranks
+    tune = tunes[0]
+    assert tune["best"] in ("route_l1", "combine") and tune["route_l1_ms"] > 0 and tune["combine_ms"] > 0, tune
+    best_is_combine = tune["best"] == "combine"
+    assert best_is_combine == (tune["combine_ms"] < tune["route_l1_ms"]), tune
+    for rank, got, _ in outs:
+        for i, (res, path, shard, plan) in enumerate(got):
+            assert path == "sorted" and plan["route_tuned"], (rank, i, plan)
+            comb = best_is_combine if i >= 4 else i >= 2
+            assert plan["combined"] == comb and plan["route_l1"] == (not comb), (rank, i, plan)
+            for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
+                assert res[f] == ref[f], (rank, i, f)
+            for a, b in zip(shard, rows):
+                assert np.array_equal(a, b[rank::2]), (rank, i)
 
 
 @pytest.mark.parametrize("name", ["drift_late", "dup_node", "r8_tombstones"])
