@@ -14,9 +14,9 @@ import csv, glob, collections, os
 f = glob.glob(f"gpurun_out/{os.environ['OUT']}/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
 for r in csv.DictReader(open(f)):
-    k = r["Kernel_Name"]
-    if "k_" not in k: continue
-    k = k.split("(")[0].replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+    k = r["Kernel_Name"].replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+    if not k.startswith("k_"): continue
+    k = k.split("(")[0]
     acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     n[(k, r["Counter_Name"])] += 1
 for k, c in acc.items():
