@@ -10,6 +10,7 @@
 #   suite : the whole -m gpu suite, then smoke()
 #   spread: the short bench in REPS processes, clocks / power per step
 #   misc  : wide-frame fan-in with flags, anchored-form PMC, flagged-form SQ counters
+#   cfgpath: cfg5 and cfg2 on each store path (gather K2 vs sorted)
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -89,6 +90,18 @@ import json; d=json.load(open('gpurun_out/${TAG}_bench_wide26.json')); w=d['with
 print('wide26', d['ms_per_step'], d['roofline']['dominant_kernel']['plan'].get('key16'), 'flags', w['ms_per_step'], w['merge_path'], w['flagged_form'], w.get('flags_equal_gather'), 'parity', (d['parity'] or {}).get('equal'))"
     CRDT_SORTED_FORM=262144 PMC_OUT=${TAG}_pmc_anchored.json bash tools/gpu_pmc_bench.sh || exit $?
     OUT=${TAG}_pmc_flags_sq bash tools/gpu_pmc_flags.sh ;;
+  cfgpath)
+    # single-changeset configs on each store path: cfg2 (10M + 10M) and cfg5 (100 streaming 10M deltas)
+    for cfg in ${CFGS:-cfg5 cfg2}; do
+      for path in gather sorted; do
+        timeout -k 10 400 python -u bench.py --config $cfg --path $path --steps 3 --warmup 1 --no-cpu --no-pcie \
+          > gpurun_out/${TAG}_${cfg}_$path.json 2> gpurun_out/${TAG}_${cfg}_$path.log
+        rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_${cfg}_$path.log; exit $rc; }
+        python3 -c "
+import json; d=json.load(open('gpurun_out/${TAG}_${cfg}_$path.json'))
+print('$cfg $path', d['ms_per_step'], d['config'].get('merge_path'), 'frac', d['roofline']['frac'], 'parity', (d.get('parity') or {}).get('equal'))"
+      done
+    done ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
