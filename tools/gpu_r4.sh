@@ -11,6 +11,7 @@
 #   spread: the short bench in REPS processes, clocks / power per step
 #   misc  : wide-frame fan-in with flags, anchored-form PMC, flagged-form SQ counters
 #   cfgpath: cfg5 and cfg2 on each store path (gather K2 vs sorted)
+#   cfg5prof: cfg5's per-call kernel / HIP API timeline (tools/ktrace_calls.py)
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -102,6 +103,16 @@ import json; d=json.load(open('gpurun_out/${TAG}_${cfg}_$path.json'))
 print('$cfg $path', d['ms_per_step'], d['config'].get('merge_path'), 'frac', d['roofline']['frac'], 'parity', (d.get('parity') or {}).get('equal'))"
       done
     done ;;
+  cfg5prof)
+    # cfg5's per-call timeline: kernel + HIP API trace of one step (100 merge calls)
+    rm -rf gpurun_out/${TAG}_prof_cfg5
+    timeout -k 10 400 rocprofv3 --kernel-trace --hip-trace --output-format csv -d gpurun_out/${TAG}_prof_cfg5 -o run \
+      -- python3 bench.py --config cfg5 --steps 1 --warmup 1 --no-cpu --no-pcie --no-census \
+      > gpurun_out/${TAG}_prof_cfg5.json 2> gpurun_out/${TAG}_prof_cfg5.log
+    rc=$?; echo "[prof] exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_cfg5.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_cfg5 -name "*kernel_trace.csv" | head -1)
+    h=$(find gpurun_out/${TAG}_prof_cfg5 -name "*hip_api_trace.csv" | head -1)
+    python3 tools/ktrace_calls.py "$k" k_apply "$h" > gpurun_out/${TAG}_cfg5_calls.txt; cat gpurun_out/${TAG}_cfg5_calls.txt ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
