@@ -1193,9 +1193,18 @@ __global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long l
 __global__ __launch_bounds__(256) void k_key_check(const uint32_t* __restrict__ key, uint64_t n, uint64_t cap,
                                                    Misc* __restrict__ misc)
 {
+    // 16-B loads over the 16-B-aligned body (a wave instruction moves 1 KB, not 256 B), scalars around it
     bool bad = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-        bad |= __builtin_nontemporal_load(key + i) >= cap;
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+    const uint64_t head = std::min<uint64_t>(n, ((16u - ((uintptr_t)key & 15u)) & 15u) / 4u);
+    const uint64_t nv = (n - head) / 4;
+    const u32x4* __restrict__ kv = reinterpret_cast<const u32x4*>(key + head);
+    for (uint64_t i = t; i < nv; i += stride) {
+        const u32x4 q = __builtin_nontemporal_load(kv + i);
+        bad |= (q.x >= cap) | (q.y >= cap) | (q.z >= cap) | (q.w >= cap);
+    }
+    if (t < head) bad |= key[t] >= cap;
+    if (head + nv * 4 + t < n) bad |= key[head + nv * 4 + t] >= cap;
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&misc->err, 1u);
 }
 
@@ -2063,7 +2072,7 @@ int apply_ranges(crdt_ctx* c, const Cols& cols, const Segs& sg, uint64_t n, int3
     // keys in under K2: there the K2 launches after the first bad id store nothing)
     c->keys_checked = !c->kv_key;
     if (c->keys_checked && n)
-        k_key_check<<<std::min<uint32_t>(grid_for(n, 256 * 16), 4096), 256, 0, c->stream>>>(cols.key, n, c->cap,
+        k_key_check<<<std::min<uint32_t>(grid_for(n, 256 * 16), 8192), 256, 0, c->stream>>>(cols.key, n, c->cap,
                                                                                            c->d_misc);
     ev_record(c, kEvApply);
     c->windows.clear();

@@ -1183,6 +1183,38 @@ def test_key_out_of_range_stores_nothing(gpu_device, path):
     t.close()
 
 
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+@pytest.mark.parametrize("where", ["first", "middle", "last"])
+def test_gather_key_check_any_alignment(gpu_device, shift, where):
+    """The gather path's up-front key check reads the keys 16 B at a time between scalar head and tail
+    elements: a bad id in the head, the body or the tail of a key column starting at any 4-B offset
+    from a 16-B boundary fails the merge with nothing stored; the same columns with good ids merge."""
+    import torch
+    from crdt_amd import CrdtNativeError, DeviceTable
+    n, cap = 4103, 1 << 16
+    rng = np.random.default_rng(shift * 7 + len(where))
+    base = torch.from_numpy(rng.permutation(cap)[: n + shift].astype(np.int32)).cuda()
+    key = base[shift:]                                          # data_ptr() at a 4 * shift offset
+    assert key.data_ptr() % 16 == (base.data_ptr() + 4 * shift) % 16
+    lt = torch.from_numpy(np.full(n, 5 << 16, np.int64)).cuda()
+    rank = torch.ones(n, dtype=torch.int32, device="cuda")
+    val = torch.zeros(n, dtype=torch.int32, device="cuda")
+    offs = np.array([0, n], np.uint64)
+    t = DeviceTable(0, local_rank=0, capacity=cap)
+    t.set_merge_path("gather")
+    t.canonical = 1 << 16
+    res, _ = t.merge(key, lt, rank, val, offs, 1 << 40, win_flags=False)
+    assert res["status"] == 0 and res["n_stored"] == n
+    t.clear_rows(0, cap)
+    i = {"first": 0, "middle": n // 2, "last": n - 1}[where]
+    key[i] = cap + 1
+    with pytest.raises(CrdtNativeError, match="key id out of range"):
+        t.merge(key, lt, rank, val, offs, 1 << 40, win_flags=False)
+    lt_r, _, _, mod = t.read_rows(np.arange(cap, dtype=np.uint32))
+    assert (mod == ABSENT_MOD).all() or (lt_r == 0).all()
+    t.close()
+
+
 def test_sorted_key_out_of_range(gpu_device):
     from crdt_amd import CrdtNativeError, DeviceTable
     t = DeviceTable(0, local_rank=0, capacity=64)
