@@ -1204,7 +1204,7 @@ def test_gather_key_check_any_alignment(gpu_device, shift, where):
     t.set_merge_path("gather")
     t.canonical = 1 << 16
     res, _ = t.merge(key, lt, rank, val, offs, 1 << 40, win_flags=False)
-    assert res["status"] == 0 and res["n_stored"] == n
+    assert res["status"] == 0 and res["n_stored"] == 1 and res["n_won"] == n
     t.clear_rows(0, cap)
     i = {"first": 0, "middle": n // 2, "last": n - 1}[where]
     key[i] = cap + 1
