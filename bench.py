@@ -336,10 +336,11 @@ def main():
         return step_ms, tsum, res
 
     # N > 1 fan-in: the library's routing tuner (comm_path.inc RouteTune) takes its trial calls — each way of
-    # moving the records twice, the faster kept — before the warmup, so every timed step takes the chosen way
+    # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4), the fastest kept — before
+    # the warmup, so every timed step takes the chosen way
     route_tune = None
     if world > 1 and args.config == "fanin" and os.environ.get("CRDT_ROUTE_TUNE", "1") != "0":
-        for _ in range(6):
+        for _ in range(8):
             reset()
             step()
             if table.route_tune()["best"] is not None:
@@ -558,11 +559,13 @@ def main():
     # packed maxima), route = plain record routing (owners run the whole sorted path); DESIGN §7
     route_ab = None
     if world > 1 and args.config == "fanin":
-        route_ab = {"default_plan": {k: v for k, v in plan.items() if k in ("route_l1", "combined", "wire_packed")}}
+        route_ab = {"default_plan": {k: v for k, v in plan.items()
+                                     if k in ("route_l1", "combined", "wire_packed", "rl1_pieces")}}
         modes = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1"},
+                 "route_l1_4": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
                  "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
                  "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"}}
-        saved = {k: os.environ.get(k) for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1")}
+        saved = {k: os.environ.get(k) for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_RL1_SPLIT")}
         for name, env in modes.items():
             os.environ.update(env)
             reset()
@@ -574,7 +577,7 @@ def main():
             p5 = table.last_plan()
             assert r5["status"] == 0 and r5["canonical_lt"] == res["canonical_lt"], (name, r5, res)
             route_ab[name] = {"ms": round(ms5, 3), "value": round(total_records / (ms5 / 1e3), 1),
-                              "route_l1": p5["route_l1"], "combined": p5["combined"]}
+                              "route_l1": p5["route_l1"], "combined": p5["combined"], "rl1_pieces": p5["rl1_pieces"]}
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)

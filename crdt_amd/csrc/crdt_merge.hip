@@ -1444,7 +1444,9 @@ struct HBuf {
 // Changeset segments of the columns an apply phase reads, in changeset order: segment s is
 // records [beg[s], end[s]) of changeset j[s].  One per changeset for a local batch; one per
 // (changeset, source rank) for records routed in by a sharded merge.
-// route_l1 (comm_path.inc): one piece's level-2 + resolve buffers at the owner (two pieces run at once)
+// route_l1 (comm_path.inc): one piece's level-2 + resolve buffers at the owner (one set per piece: the
+// host writes a piece's plan while earlier pieces' copies may still be queued)
+constexpr uint32_t kRl1MaxPieces = 4;
 struct Rl1Scratch {
     DBuf<uint32_t> hist, toff, part, choff, dstart2, tseg, ibase, ibucket, ksu32, kj2;
     DBuf<int64_t> kslt;
@@ -1596,7 +1598,9 @@ struct crdt_ctx {
     bool last_combined = false;
     uint32_t sparse_t = 1024;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
     bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
-    bool rl1_split = true;          // CRDT_RL1_SPLIT=0: route_l1 partitions and sends in one piece
+    uint32_t rl1_pieces = 2;        // CRDT_RL1_SPLIT: route_l1's pipelined pieces (0 / 1: one; up to kRl1MaxPieces)
+    uint32_t rl1_call_pieces = 2;   // ... this call's (the tuner's way 2 takes kRl1MaxPieces)
+    uint32_t last_rl1_pieces = 0;   // ... the last routed merge's
     bool last_route_l1 = false;     // the last sharded merge partitioned its home records into the owners' buckets
     // the routing of a sharded order-free fan-in, measured (comm_path.inc, RouteTune): route_l1 sends 14-B
     // partition records, the combine folds first and sends ~3.4x fewer bytes at more local work; which is
@@ -1605,8 +1609,8 @@ struct crdt_ctx {
     struct RouteTune {
         uint64_t shape = 0;         // (R, G, cap) the trials were taken for
         uint32_t trial = 0;         // trial calls taken (kTrials per way)
-        int best = -1;              // 0 route_l1, 1 combine; -1 while trials run
-        long long us[2] = {-1, -1}; // each way's second call, max over ranks (microseconds)
+        int best = -1;              // 0 route_l1 in 2 pieces, 1 combine, 2 route_l1 in 4; -1 while trials run
+        long long us[3] = {-1, -1, -1};   // each way's second call, max over ranks (microseconds)
     } rt;
     int tune_mode = -1;             // this call's way from the tuner (-1: the fixed rule)
     bool tune_trial = false;        // ... and the call took it with both ways open (a trial / a tuned call)
@@ -1615,7 +1619,7 @@ struct crdt_ctx {
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
     DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
     uint64_t rl_cap = 0;            // records both hold
-    Rl1Scratch rl_os[2];            // the owner's level 2 + resolve of each piece
+    Rl1Scratch rl_os[kRl1MaxPieces];   // the owner's level 2 + resolve of each piece
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
@@ -1645,8 +1649,11 @@ struct crdt_ctx {
     DBuf<unsigned long long> d_rcnt, d_rrecv;             // [G][R] route counts sent / received
     DBuf<unsigned long long> d_rcur;                      // [G][R] scatter cursors (k_route_plan)
     hipEvent_t route_ev = nullptr;                        // the route counts have reached the host
-    hipStream_t sstream = nullptr;                        // route_l1: the second half's partition
-    hipEvent_t rl_ev[4] = {};       // route_l1: piece 0 / 1 partitioned, piece 0 exchanged, piece 0 resolved
+    hipStream_t sstream = nullptr;                        // route_l1: the partition of pieces 1 .. P-1
+    hipStream_t ostream = nullptr;                        // route_l1: the owner work of pieces 0 .. P-2
+    hipEvent_t rl_evs[kRl1MaxPieces] = {};                // route_l1: piece q partitioned
+    hipEvent_t rl_evx[kRl1MaxPieces] = {};                // ... piece q exchanged
+    hipEvent_t rl_evo = nullptr;                          // ... pieces 0 .. P-2 resolved at the owner
     uint64_t recv_cap = 0;                                // receive columns' capacity (records)
     HBuf<uint64_t> h_rcnt;                                // both, read back once per call
     DBuf<uint32_t> r_skey, r_srank, r_sval, r_key, r_rank, r_val;   // send / receive columns
@@ -2883,7 +2890,10 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_RL1_SPLIT")) c->rl1_split = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_RL1_SPLIT")) {   // 0: one piece, 1: two (the default), n: n pieces
+        const int v = atoi(e);
+        c->rl1_pieces = std::min<uint32_t>(v <= 0 ? 1u : v == 1 ? 2u : (uint32_t)v, kRl1MaxPieces);
+    }
     if (const char* e = getenv("CRDT_ROUTE_TUNE")) c->route_tune = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
     if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
@@ -2948,8 +2958,11 @@ void crdt_destroy(crdt_ctx* c) {
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
     c->d_rcur.release();
     if (c->route_ev) hipEventDestroy(c->route_ev);
-    for (hipEvent_t e : c->rl_ev) if (e) hipEventDestroy(e);
+    for (hipEvent_t e : c->rl_evs) if (e) hipEventDestroy(e);
+    for (hipEvent_t e : c->rl_evx) if (e) hipEventDestroy(e);
+    if (c->rl_evo) hipEventDestroy(c->rl_evo);
     if (c->sstream) hipStreamDestroy(c->sstream);
+    if (c->ostream) hipStreamDestroy(c->ostream);
     if (c->table.base) hipFree(c->table.base);
     if (c->d_misc) hipFree(c->d_misc);
     if (c->h_misc) hipHostFree(c->h_misc);
@@ -2974,7 +2987,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->e_key.release(); c->e_val.release(); c->e_pk.release(); c->e_cnt.release(); c->e_cur.release();
     c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
     c->h_ebase.release();
-    c->rl_rec.release(); c->rl_k16.release(); c->rl_os[0].release(); c->rl_os[1].release();
+    c->rl_rec.release(); c->rl_k16.release(); for (Rl1Scratch& os : c->rl_os) os.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
@@ -3364,6 +3377,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;
     if (c->tune_trial) f |= CRDT_PLAN_ROUTE_TUNED;
+    if (c->last_route_l1) f |= (c->last_rl1_pieces & 7u) << CRDT_PLAN_RL1_PIECES_SHIFT;
     *flags = f;
     return CRDT_OK;
 }
@@ -3371,8 +3385,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
 int crdt_route_tune_info(const crdt_ctx* c, int32_t* best, int64_t* us) {
     if (!c || !best || !us) return CRDT_E_INVALID;
     *best = c->rt.best;
-    us[0] = c->rt.us[0];
-    us[1] = c->rt.us[1];
+    for (int w = 0; w < 3; ++w) us[w] = c->rt.us[w];
     return CRDT_OK;
 }
 

@@ -318,17 +318,23 @@ class DeviceTable:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""
         v = ctypes.c_uint32(0)
         self._check(self._lib.crdt_last_plan(self._ctx, ctypes.byref(v)), "crdt_last_plan")
-        return {k: bool(v.value & b) for k, b in self.PLAN_FLAGS.items()}
+        plan = {k: bool(v.value & b) for k, b in self.PLAN_FLAGS.items()}
+        plan["rl1_pieces"] = (v.value >> 15) & 7                # route_l1's pipelined pieces (0: not route_l1)
+        return plan
+
+    TUNE_WAYS = ("route_l1", "combine", "route_l1_4")
 
     def route_tune(self) -> dict:
         """crdt_route_tune_info: the sharded fan-in routing the ctx measured ({'best': None while the
-        trials run, else 'route_l1' / 'combine'; 'route_l1_ms' / 'combine_ms': each way's timed call,
-        max over ranks, None if not yet})."""
+        trials run, else 'route_l1' (2 pipelined pieces) / 'combine' / 'route_l1_4' (4 pieces);
+        '<way>_ms': each way's timed call, max over ranks, None if not yet})."""
         best = ctypes.c_int32(0)
-        us = (ctypes.c_int64 * 2)()
+        us = (ctypes.c_int64 * 3)()
         self._check(self._lib.crdt_route_tune_info(self._ctx, ctypes.byref(best), us), "crdt_route_tune_info")
-        ms = [u / 1e3 if u >= 0 else None for u in us]
-        return {"best": {0: "route_l1", 1: "combine"}.get(best.value), "route_l1_ms": ms[0], "combine_ms": ms[1]}
+        out = {"best": self.TUNE_WAYS[best.value] if 0 <= best.value < 3 else None}
+        for w, u in zip(self.TUNE_WAYS, us):
+            out[f"{w}_ms"] = u / 1e3 if u >= 0 else None
+        return out
 
     def set_timing(self, enable: bool):
         self._check(self._lib.crdt_set_timing(self._ctx, int(bool(enable))), "crdt_set_timing")

@@ -294,18 +294,19 @@ enum crdt_plan_flags {
     CRDT_PLAN_ROUTE_L1 = 8192,   /* sharded ctx: home records partitioned once, straight into their owners'
                                     level-1 buckets; 14-B level-1 records crossed the exchange and the
                                     owners started at level 2 (comm_path.inc, route_l1) */
-    CRDT_PLAN_ROUTE_TUNED = 16384 /* sharded ctx: the way (route_l1 or the combine) came from the routing
+    CRDT_PLAN_ROUTE_TUNED = 16384, /* sharded ctx: the way (route_l1 or the combine) came from the routing
                                     tuner, a trial or its measured choice (crdt_route_tune_info) */
+    CRDT_PLAN_RL1_PIECES_SHIFT = 15 /* bits 15-17: route_l1's pipelined pieces (1-4; 0: not route_l1) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 
 /* Sharded ctx: the measured routing of order-free many-changeset fan-ins (comm_path.inc, RouteTune;
- * CRDT_ROUTE_TUNE=0 turns it off).  While both ways are open (the auto settings), the first calls take each
+ * CRDT_ROUTE_TUNE=0 turns it off).  While every way is open (the auto settings), the first calls take each
  * way twice, the second call of each timed on the host and MAX-reduced over the ranks; later calls with the
- * same (changesets, ranks, capacity) take the faster.  *best: -1 while the trials run (or before any such
- * call), 0 = route_l1, 1 = the map-side combine; us[0] / us[1]: their timed calls in microseconds (-1: not
- * yet).  Every way leaves the same rows. */
-int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us);
+ * same (changesets, ranks, capacity) take the fastest.  *best: -1 while the trials run (or before any such
+ * call), 0 = route_l1 in 2 pipelined pieces, 1 = the map-side combine, 2 = route_l1 in 4 pieces;
+ * us[0 .. 2]: their timed calls in microseconds (-1: not yet).  Every way leaves the same rows. */
+int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [3] */);
 
 /* ---- measurement ---------------------------------------------------------- */
 int crdt_set_timing(crdt_ctx* ctx, int enable);

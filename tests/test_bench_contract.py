@@ -73,5 +73,6 @@ def test_bench_two_ranks_routed(gpu_device):
     assert ab["combine"]["combined"] and not ab["route"]["route_l1"] and not ab["route"]["combined"]
     assert all(ab[m]["ms"] > 0 for m in ("route_l1", "combine", "route"))
     tune = d["route_tune"]                                      # the way every timed step took, measured
-    assert tune["best"] in ("route_l1", "combine") and tune["route_l1_ms"] > 0 and tune["combine_ms"] > 0
+    assert tune["best"] in ("route_l1", "combine", "route_l1_4")
+    assert all(tune[f"{w}_ms"] > 0 for w in ("route_l1", "combine", "route_l1_4"))
     assert ab["default_plan"]["combined"] == (tune["best"] == "combine")

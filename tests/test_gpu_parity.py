@@ -567,7 +567,8 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R, calls=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("combine,route_l1,split", [("1", "1", "1"), ("0", "1", "1"), ("0", "1", "0"), ("0", "0", "1")])
+@pytest.mark.parametrize("combine,route_l1,split", [("1", "1", "1"), ("0", "1", "1"), ("0", "1", "0"), ("0", "1", "4"),
+                                                    ("0", "1", "3"), ("0", "0", "1")])
 def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1, split):
     """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
     routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
@@ -609,6 +610,8 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
         assert path == "sorted"
         assert plan["combined"] == (combine == "1"), plan
         assert plan["route_l1"] == (combine == "0" and route_l1 == "1"), plan
+        if plan["route_l1"]:                                   # pieces cut at changeset boundaries
+            assert plan["rl1_pieces"] == {"0": 1, "1": 2}.get(split, int(split)), plan
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
             assert res[f] == ref[f], (rank, f)
         for a, b in zip(shard, rows):
@@ -633,9 +636,10 @@ def _fanin_reference(K, total, R):
 
 
 def test_two_rank_route_tune(gpu_device, monkeypatch):
-    """The routing tuner (comm_path.inc RouteTune, the auto settings): the first calls take route_l1 twice
-    and the map-side combine twice, every later call the way whose timed call was faster (max over the
-    ranks, the same way on both ranks); every call leaves exactly the unsharded merge's rows."""
+    """The routing tuner (comm_path.inc RouteTune, the auto settings): the first calls take route_l1 in two
+    pieces twice, the map-side combine twice and route_l1 in four pieces twice, every later call the way
+    whose timed call was fastest (max over the ranks, the same way on both ranks); every call leaves
+    exactly the unsharded merge's rows."""
     for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_ROUTE_TUNE", "CRDT_RL1_SPLIT"):
         monkeypatch.delenv(k, raising=False)
     import torch.multiprocessing as mp
@@ -646,7 +650,7 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 6)) for r in range(2)]
+    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 8)) for r in range(2)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
@@ -656,14 +660,16 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     tunes = [o[2] for o in outs]
     assert tunes[0] == tunes[1], tunes                        # one decision, from the max over ranks
     tune = tunes[0]
-    assert tune["best"] in ("route_l1", "combine") and tune["route_l1_ms"] > 0 and tune["combine_ms"] > 0, tune
-    best_is_combine = tune["best"] == "combine"
-    assert best_is_combine == (tune["combine_ms"] < tune["route_l1_ms"]), tune
+    ways = ("route_l1", "combine", "route_l1_4")
+    assert tune["best"] in ways and all(tune[f"{w}_ms"] > 0 for w in ways), tune
+    assert tune["best"] == min(ways, key=lambda w: tune[f"{w}_ms"]), tune
     for rank, got, _ in outs:
         for i, (res, path, shard, plan) in enumerate(got):
             assert path == "sorted" and plan["route_tuned"], (rank, i, plan)
-            comb = best_is_combine if i >= 4 else i >= 2
-            assert plan["combined"] == comb and plan["route_l1"] == (not comb), (rank, i, plan)
+            way = tune["best"] if i >= 6 else ways[i // 2]
+            assert plan["combined"] == (way == "combine") and plan["route_l1"] == (way != "combine"), (rank, i, plan)
+            if way != "combine":
+                assert plan["rl1_pieces"] == (4 if way == "route_l1_4" else 2), (rank, i, plan)
             for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
                 assert res[f] == ref[f], (rank, i, f)
             for a, b in zip(shard, rows):

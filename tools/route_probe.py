@@ -28,10 +28,11 @@ from crdt_amd.workload import gen_fanin  # noqa: E402
 
 N = int(os.environ.get("N", "8"))
 STEPS = int(os.environ.get("STEPS", "3"))
-MODES = os.environ.get("MODES", "route_l1,route_l1_1piece,route,combine").split(",")
+MODES = os.environ.get("MODES", "route_l1,route_l1_1piece,route_l1_4piece,route,combine").split(",")
 os.environ["CRDT_ENV_DYNAMIC"] = "1"
 ENV = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "1"},
        "route_l1_1piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "0"},
+       "route_l1_4piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
        "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"},
        "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"}}
 
