@@ -336,11 +336,11 @@ def main():
         return step_ms, tsum, res
 
     # N > 1 fan-in: the library's routing tuner (comm_path.inc RouteTune) takes its trial calls — each way of
-    # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4), the fastest kept — before
+    # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4 and in 1), the fastest kept — before
     # the warmup, so every timed step takes the chosen way
     route_tune = None
     if world > 1 and args.config == "fanin" and os.environ.get("CRDT_ROUTE_TUNE", "1") != "0":
-        for _ in range(8):
+        for _ in range(10):
             reset()
             step()
             if table.route_tune()["best"] is not None:

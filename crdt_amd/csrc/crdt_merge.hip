@@ -1609,8 +1609,9 @@ struct crdt_ctx {
     struct RouteTune {
         uint64_t shape = 0;         // (R, G, cap) the trials were taken for
         uint32_t trial = 0;         // trial calls taken (kTrials per way)
-        int best = -1;              // 0 route_l1 in 2 pieces, 1 combine, 2 route_l1 in 4; -1 while trials run
-        long long us[3] = {-1, -1, -1};   // each way's second call, max over ranks (microseconds)
+        int best = -1;              // 0 route_l1 in 2 pieces, 1 combine, 2 route_l1 in 4, 3 route_l1 in 1;
+                                    // -1 while the trials run
+        long long us[4] = {-1, -1, -1, -1};   // each way's second call, max over ranks (microseconds)
     } rt;
     int tune_mode = -1;             // this call's way from the tuner (-1: the fixed rule)
     bool tune_trial = false;        // ... and the call took it with both ways open (a trial / a tuned call)
@@ -3385,7 +3386,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
 int crdt_route_tune_info(const crdt_ctx* c, int32_t* best, int64_t* us) {
     if (!c || !best || !us) return CRDT_E_INVALID;
     *best = c->rt.best;
-    for (int w = 0; w < 3; ++w) us[w] = c->rt.us[w];
+    for (int w = 0; w < 4; ++w) us[w] = c->rt.us[w];
     return CRDT_OK;
 }
 

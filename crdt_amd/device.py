@@ -322,16 +322,16 @@ class DeviceTable:
         plan["rl1_pieces"] = (v.value >> 15) & 7                # route_l1's pipelined pieces (0: not route_l1)
         return plan
 
-    TUNE_WAYS = ("route_l1", "combine", "route_l1_4")
+    TUNE_WAYS = ("route_l1", "combine", "route_l1_4", "route_l1_1")
 
     def route_tune(self) -> dict:
         """crdt_route_tune_info: the sharded fan-in routing the ctx measured ({'best': None while the
-        trials run, else 'route_l1' (2 pipelined pieces) / 'combine' / 'route_l1_4' (4 pieces);
+        trials run, else 'route_l1' (2 pipelined pieces) / 'combine' / 'route_l1_4' (4) / 'route_l1_1' (1);
         '<way>_ms': each way's timed call, max over ranks, None if not yet})."""
         best = ctypes.c_int32(0)
-        us = (ctypes.c_int64 * 3)()
+        us = (ctypes.c_int64 * 4)()
         self._check(self._lib.crdt_route_tune_info(self._ctx, ctypes.byref(best), us), "crdt_route_tune_info")
-        out = {"best": self.TUNE_WAYS[best.value] if 0 <= best.value < 3 else None}
+        out = {"best": self.TUNE_WAYS[best.value] if 0 <= best.value < 4 else None}
         for w, u in zip(self.TUNE_WAYS, us):
             out[f"{w}_ms"] = u / 1e3 if u >= 0 else None
         return out

@@ -304,9 +304,10 @@ int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
  * CRDT_ROUTE_TUNE=0 turns it off).  While every way is open (the auto settings), the first calls take each
  * way twice, the second call of each timed on the host and MAX-reduced over the ranks; later calls with the
  * same (changesets, ranks, capacity) take the fastest.  *best: -1 while the trials run (or before any such
- * call), 0 = route_l1 in 2 pipelined pieces, 1 = the map-side combine, 2 = route_l1 in 4 pieces;
- * us[0 .. 2]: their timed calls in microseconds (-1: not yet).  Every way leaves the same rows. */
-int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [3] */);
+ * call), 0 = route_l1 in 2 pipelined pieces, 1 = the map-side combine, 2 = route_l1 in 4 pieces,
+ * 3 = route_l1 in one; us[0 .. 3]: their timed calls in microseconds (-1: not yet).  Every way leaves the
+ * same rows. */
+int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [4] */);
 
 /* ---- measurement ---------------------------------------------------------- */
 int crdt_set_timing(crdt_ctx* ctx, int enable);

@@ -637,7 +637,7 @@ def _fanin_reference(K, total, R):
 
 def test_two_rank_route_tune(gpu_device, monkeypatch):
     """The routing tuner (comm_path.inc RouteTune, the auto settings): the first calls take route_l1 in two
-    pieces twice, the map-side combine twice and route_l1 in four pieces twice, every later call the way
+    pieces twice, the map-side combine twice, route_l1 in four pieces and in one twice each, every later call the way
     whose timed call was fastest (max over the ranks, the same way on both ranks); every call leaves
     exactly the unsharded merge's rows."""
     for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_ROUTE_TUNE", "CRDT_RL1_SPLIT"):
@@ -650,7 +650,7 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 8)) for r in range(2)]
+    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 10)) for r in range(2)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
@@ -660,16 +660,16 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     tunes = [o[2] for o in outs]
     assert tunes[0] == tunes[1], tunes                        # one decision, from the max over ranks
     tune = tunes[0]
-    ways = ("route_l1", "combine", "route_l1_4")
+    ways = ("route_l1", "combine", "route_l1_4", "route_l1_1")
     assert tune["best"] in ways and all(tune[f"{w}_ms"] > 0 for w in ways), tune
     assert tune["best"] == min(ways, key=lambda w: tune[f"{w}_ms"]), tune
     for rank, got, _ in outs:
         for i, (res, path, shard, plan) in enumerate(got):
             assert path == "sorted" and plan["route_tuned"], (rank, i, plan)
-            way = tune["best"] if i >= 6 else ways[i // 2]
+            way = tune["best"] if i >= 8 else ways[i // 2]
             assert plan["combined"] == (way == "combine") and plan["route_l1"] == (way != "combine"), (rank, i, plan)
             if way != "combine":
-                assert plan["rl1_pieces"] == (4 if way == "route_l1_4" else 2), (rank, i, plan)
+                assert plan["rl1_pieces"] == {"route_l1_4": 4, "route_l1_1": 1}.get(way, 2), (rank, i, plan)
             for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
                 assert res[f] == ref[f], (rank, i, f)
             for a, b in zip(shard, rows):
