@@ -618,6 +618,55 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
             assert np.array_equal(a, b[rank::2]), rank
 
 
+@pytest.mark.parametrize("G", [4, 8])
+def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
+    """The device-memory collective path — the one RCCL takes: no host synchronisation inside the
+    collectives, so the partition, the exchanges and the owners' work overlap on their three streams as
+    they do on the node — on one GPU through a loopback communicator (tests/_loopback.py: rank 0 of G ranks
+    that all hold its data; the peers' parts come back as device copies).  route_l1 in 1, 2, 3 and 4
+    pipelined pieces, record routing and the map-side fold apply the same records and must leave the same
+    rows.  (Under the loopback, keys of different owners share rank 0's slots, so two records of one slot
+    may carry equal packed keys and the order-free fold may keep either value: lt / rank / mod must match
+    exactly, val in all but a handful of such tie slots.)"""
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    from tests._loopback import LoopbackComm
+    monkeypatch.setenv("CRDT_ENV_DYNAMIC", "1")
+    wl = gen_fanin(total=8_000_000, R=128, K=1 << 24, n_local=1 << 23, s=0.8, device="cuda", rank=0, world=G,
+                   route=True)
+    home, loc, cap = wl["home"], wl["local"], wl["capacity"]
+    t = DeviceTable(0, local_rank=0, capacity=cap)
+    t.set_counts(False)
+    comm = LoopbackComm(G)
+    t.comm_init_ops(G, 0, comm)
+    ways = {"1": ("0", "1", "0", 1), "2": ("0", "1", "1", 2), "3": ("0", "1", "3", 3), "4": ("0", "1", "4", 4),
+            "route": ("0", "0", "1", 0), "fold": ("2", "1", "1", 0)}
+    rows = {}
+    for name, (comb, rl1, split, pieces) in ways.items():
+        monkeypatch.setenv("CRDT_COMBINE", comb)
+        monkeypatch.setenv("CRDT_ROUTE_L1", rl1)
+        monkeypatch.setenv("CRDT_RL1_SPLIT", split)
+        for _ in range(2):                                    # (the second call reuses every buffer)
+            t.clear_rows(0, cap)
+            t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+            t.canonical = wl["c0"]
+            res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
+                             win_flags=False)
+            assert res["status"] == 0 and comm.error is None, (name, res, comm.error)
+            plan = t.last_plan()
+            assert plan["route_l1"] == (pieces > 0) and plan["rl1_pieces"] == pieces, (name, plan)
+            assert plan["combined"] == (name == "fold"), (name, plan)
+            rows.setdefault(name, []).append(t.read_rows(np.arange(cap, dtype=np.uint32)))
+    comm.exchange_ms()
+    t.close()
+    ref = rows["1"][0]
+    for name, runs in rows.items():
+        for got in runs:                                      # (each way twice: the second reuses every buffer)
+            for f in (0, 1, 3):
+                assert np.array_equal(ref[f], got[f]), (name, f)
+            assert int((ref[2] != got[2]).sum()) <= 16, name
+
+
 def _fanin_reference(K, total, R):
     """The unsharded K2 merge of gen_fanin's whole job: (result, all rows)."""
     from crdt_amd import DeviceTable

@@ -14,7 +14,6 @@ path), combine (map-side fold first).  Prints per mode the merge's device time, 
 time, local work = the difference, and the library's phase split; then checks that the modes leave the
 same rows (lt, rank, mod everywhere; val except where two same-slot records carry equal packed keys —
 counted and printed).  ENV: N (default 8), STEPS (per mode, default 3), MODES (default all three)."""
-import ctypes
 import os
 import sys
 import time
@@ -23,8 +22,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from crdt_amd import DeviceTable, _capi  # noqa: E402
+from crdt_amd import DeviceTable  # noqa: E402
 from crdt_amd.workload import gen_fanin  # noqa: E402
+from tests._loopback import LoopbackComm  # noqa: E402
 
 N = int(os.environ.get("N", "8"))
 STEPS = int(os.environ.get("STEPS", "3"))
@@ -35,78 +35,6 @@ ENV = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT":
        "route_l1_4piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
        "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"},
        "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"}}
-
-hip = ctypes.CDLL("libamdhip64.so.7")
-hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
-hip.hipEventCreate.argtypes = [ctypes.c_void_p]
-hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
-hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
-D2D = 3
-
-
-class LoopbackComm:
-    """crdt_comm_ops (device memory) for rank 0 of G ranks that all hold rank 0's data."""
-
-    def __init__(self, G):
-        self.G = G
-        self.error = None
-        self.evs = []                                  # (start, end) events around each record exchange
-
-    def _event(self):
-        e = ctypes.c_void_p()
-        assert hip.hipEventCreate(ctypes.byref(e)) == 0
-        return e
-
-    def exchange_ms(self):
-        ms, tot = ctypes.c_float(), 0.0
-        for a, b in self.evs:
-            hip.hipEventSynchronize(b)
-            hip.hipEventElapsedTime(ctypes.byref(ms), a, b)
-            tot += ms.value
-        self.evs = []
-        return tot
-
-    def ops(self):
-        G = self
-
-        def guard(fn):
-            def call(*a):
-                try:
-                    return fn(*a)
-                except Exception as e:  # noqa: BLE001
-                    G.error = e
-                    return 1
-            return call
-
-        def _ar(user, words, n, op, stream):
-            return 0                                   # identical words on every rank
-
-        def _ag(user, send, recv, n, stream):
-            for r in range(G.G):
-                assert hip.hipMemcpyAsync(recv + r * n * 8, send, n * 8, D2D, stream) == 0
-            return 0
-
-        def _a2a(user, n_cols, send, recv, eb, sc, sd, rc, rd, stream):
-            big = sum(sc[d] * eb[k] for d in range(G.G) for k in range(n_cols)) > (1 << 20)
-            if big:
-                a, b = G._event(), G._event()
-                hip.hipEventRecord(a, stream)
-            for d in range(G.G):
-                for k in range(n_cols):
-                    nb = min(sc[d], rc[d]) * eb[k]
-                    if nb:
-                        assert hip.hipMemcpyAsync(recv[k] + rd[d] * eb[k], send[k] + sd[d] * eb[k], nb, D2D,
-                                                  stream) == 0
-            if big:
-                hip.hipEventRecord(b, stream)
-                G.evs.append((a, b))
-            return 0
-
-        self._cbs = (_capi.ALL_REDUCE_FN(guard(_ar)), _capi.ALL_GATHER_FN(guard(_ag)),
-                     _capi.ALL_TO_ALL_FN(guard(_a2a)))
-        return _capi.CrdtCommOps(None, _capi.CRDT_MEM_DEVICE, 0, *self._cbs)
-
 
 wl = gen_fanin(total=1_000_000_512, R=1024, K=1 << 28, n_local=1 << 27, s=0.8, device="cuda", rank=0, world=N,
                route=True)
