@@ -632,7 +632,7 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
     from crdt_amd.workload import gen_fanin
     from tests._loopback import LoopbackComm
     monkeypatch.setenv("CRDT_ENV_DYNAMIC", "1")
-    wl = gen_fanin(total=8_000_000, R=128, K=1 << 24, n_local=1 << 23, s=0.8, device="cuda", rank=0, world=G,
+    wl = gen_fanin(total=2_000_000 * G, R=128, K=1 << 24, n_local=1 << 23, s=0.8, device="cuda", rank=0, world=G,
                    route=True)
     home, loc, cap = wl["home"], wl["local"], wl["capacity"]
     t = DeviceTable(0, local_rank=0, capacity=cap)
