@@ -39,9 +39,10 @@ case "${STAGE:-flags}" in
       rc=$?; grep -E "mean|rows|home" gpurun_out/${TAG}_probe_n$n.log; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_probe_n$n.log; exit $rc; }
     done ;;
   cfg3)
-    timeout -k 10 500 python -u bench.py --config cfg3 --steps 8 --warmup 2 --no-cpu --no-pcie --ab CRDT_SPARSE_T=0,1024 \
-      > gpurun_out/${TAG}_cfg3_ab.json 2> gpurun_out/${TAG}_cfg3_ab.log
+    timeout -k 10 500 python -u bench.py --config cfg3 --steps ${STEPS:-8} --warmup 2 --no-cpu --no-pcie \
+      --ab ${AB:-CRDT_SPARSE_T=0,1024} > gpurun_out/${TAG}_cfg3_ab.json 2> gpurun_out/${TAG}_cfg3_ab.log
     rc=$?; grep "A/B" gpurun_out/${TAG}_cfg3_ab.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_cfg3_ab.log; exit $rc; }
+    [ -n "${NO_PMC:-}" ] && exit 0
     ARGS="--config cfg3 --steps 1 --warmup 0 --no-cpu --no-census --no-pcie" MERGES=1 PMC_OUT=${TAG}_pmc_cfg3.json \
       bash tools/gpu_pmc_bench.sh ;;
   fprof)
