@@ -1596,7 +1596,7 @@ struct crdt_ctx {
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
     bool last_combined = false;
-    uint32_t sparse_t = 1024;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
+    uint32_t sparse_t = 2048;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
     bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
     uint32_t rl1_pieces = 2;        // CRDT_RL1_SPLIT: route_l1's pipelined pieces (0 / 1: one; up to kRl1MaxPieces)
     uint32_t rl1_call_pieces = 2;   // ... this call's (the tuner's way 2 takes kRl1MaxPieces)
