@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -1404,16 +1405,108 @@ static bool contig_alloc() {
     return v != 0;
 }
 
+// CRDT_ALLOC_SHUFFLE=1: the partition buffers are assembled from separately created physical chunks of
+// CRDT_SHUFFLE_KB (default 2048) mapped into one virtual range in a fixed pseudo-random order (the HIP
+// virtual-memory API), so their physical placement no longer depends on the allocator's state — the second
+// placement experiment of DESIGN §6.  Freed through vmm_free (DBuf::vmm).
+struct VmmRange {
+    size_t bytes = 0;
+    std::vector<hipMemGenericAllocationHandle_t> chunks;
+};
+static std::mutex g_vmm_mu;
+static std::vector<std::pair<void*, VmmRange>> g_vmm;
+
+static bool shuffle_alloc() {
+    static const int v = [] { const char* e = getenv("CRDT_ALLOC_SHUFFLE"); return e && atoi(e) ? 1 : 0; }();
+    return v != 0;
+}
+
+static hipError_t vmm_shuffled_alloc(void** out, size_t bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    if ((e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum)) != hipSuccess) return e;
+    size_t chunk = (size_t)2 << 20;
+    if (const char* v = getenv("CRDT_SHUFFLE_KB")) chunk = (size_t)std::max(atoi(v), 4) << 10;
+    chunk = (chunk + gran - 1) / gran * gran;
+    const size_t nch = (bytes + chunk - 1) / chunk, total = nch * chunk;
+    void* va = nullptr;
+    if ((e = hipMemAddressReserve(&va, total, chunk, nullptr, 0)) != hipSuccess) return e;
+    VmmRange r;
+    r.bytes = total;
+    std::vector<size_t> perm(nch);
+    for (size_t i = 0; i < nch; ++i) perm[i] = i;
+    uint64_t x = 0x9E3779B97F4A7C15ull ^ nch;                      // fixed order (splitmix64 Fisher-Yates)
+    for (size_t i = nch; i > 1; --i) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        std::swap(perm[i - 1], perm[z % i]);
+    }
+    for (size_t i = 0; i < nch && e == hipSuccess; ++i) {
+        hipMemGenericAllocationHandle_t h;
+        if ((e = hipMemCreate(&h, chunk, &prop, 0)) != hipSuccess) break;
+        r.chunks.push_back(h);
+        e = hipMemMap(static_cast<char*>(va) + perm[i] * chunk, chunk, 0, h, 0);
+    }
+    if (e == hipSuccess) {
+        hipMemAccessDesc acc{};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(va, total, &acc, 1);
+    }
+    if (e != hipSuccess) {
+        hipMemUnmap(va, total);
+        for (auto h : r.chunks) hipMemRelease(h);
+        hipMemAddressFree(va, total);
+        return e;
+    }
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    g_vmm.emplace_back(va, std::move(r));
+    *out = va;
+    return hipSuccess;
+}
+
+static void vmm_free(void* va) {
+    VmmRange r;
+    {
+        std::lock_guard<std::mutex> g(g_vmm_mu);
+        for (size_t i = 0; i < g_vmm.size(); ++i)
+            if (g_vmm[i].first == va) {
+                r = std::move(g_vmm[i].second);
+                g_vmm.erase(g_vmm.begin() + (ptrdiff_t)i);
+                break;
+            }
+    }
+    if (!r.bytes) return;
+    hipDeviceSynchronize();                         // (hipFree's implicit wait, which unmapping lacks)
+    hipMemUnmap(va, r.bytes);
+    for (auto h : r.chunks) hipMemRelease(h);
+    hipMemAddressFree(va, r.bytes);
+}
+
 template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
+    bool vmm = false;               // p came from vmm_shuffled_alloc
     hipError_t ensure(size_t want, bool contig = false) {
         if (want <= n && p) return hipSuccess;
-        if (p) { hipFree(p); p = nullptr; n = 0; }
+        if (p) release();
         size_t m = std::max<size_t>(want, 16);
         hipError_t e = hipErrorMemoryAllocation;
-        if (contig && contig_alloc())
+        if (contig && shuffle_alloc()) {
+            e = vmm_shuffled_alloc(reinterpret_cast<void**>(&p), m * sizeof(T));
+            vmm = e == hipSuccess;
+        }
+        if (e != hipSuccess && contig && contig_alloc())
             e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p), m * sizeof(T), hipDeviceMallocContiguous);
         if (e != hipSuccess) e = hipMalloc(&p, m * sizeof(T));
         if (e == hipSuccess) n = m;
@@ -1423,7 +1516,13 @@ struct DBuf {
         }
         return e;
     }
-    void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+    void release() {
+        if (p && vmm) vmm_free(p);
+        else if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+        vmm = false;
+    }
 };
 
 template <typename T>
