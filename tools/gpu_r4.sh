@@ -12,6 +12,7 @@
 #   misc  : wide-frame fan-in with flags, anchored-form PMC, flagged-form SQ counters
 #   cfgpath: cfg5 and cfg2 on each store path (gather K2 vs sorted)
 #   cfg5prof: cfg5's per-call kernel / HIP API timeline (tools/ktrace_calls.py)
+#   place : the level-1 scatter per allocation of the partition buffers (tools/place_probe.py)
 #   ab    : in-process A/B of the 1B flagged merge (AB="VAR=a,b")
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -115,6 +116,10 @@ print('$cfg $path', d['ms_per_step'], d['config'].get('merge_path'), 'frac', d['
     k=$(find gpurun_out/${TAG}_prof_cfg5 -name "*kernel_trace.csv" | head -1)
     h=$(find gpurun_out/${TAG}_prof_cfg5 -name "*hip_api_trace.csv" | head -1)
     python3 tools/ktrace_calls.py "$k" k_apply "$h" > gpurun_out/${TAG}_cfg5_calls.txt; cat gpurun_out/${TAG}_cfg5_calls.txt ;;
+  place)
+    # the level-1 scatter per allocation of the partition buffers, in one process (tools/place_probe.py)
+    A=${A:-5} STEPS=${STEPS:-3} timeout -k 10 500 python -u tools/place_probe.py > gpurun_out/${TAG}_place.log 2>&1
+    rc=$?; grep allocation gpurun_out/${TAG}_place.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_place.log; exit $rc; } ;;
   ab)
     STEPS=${STEPS:-9} timeout -k 10 400 python -u tools/prof_flags.py > gpurun_out/${TAG}_flags_ab.log 2>&1
     rc=$?; grep -E "A/B|step" gpurun_out/${TAG}_flags_ab.log | tail -12; exit $rc ;;
