@@ -347,6 +347,20 @@ def main():
                 break
         route_tune = table.route_tune()
         log(f"routing tuner: {route_tune}")
+    # N = 1 fan-in: the library's placement tuner (crdt_reserve_scratch took candidate level-1 buffers) times
+    # the level-1 scatter on each in the first merges and keeps the fastest — also before the warmup
+    placement = None
+    if world == 1 and table.place_info()["candidates"] > 1:
+        for _ in range(6):
+            before = table.place_info()
+            if before["kept"] is not None:
+                break
+            reset()
+            step()
+            if table.place_info() == before:            # (this path does not partition: nothing to time)
+                break
+        placement = table.place_info()
+        log(f"placement tuner: {placement}")
     for _ in range(args.warmup):
         reset()
         step()
@@ -635,7 +649,7 @@ def main():
                    "step_ms_all": [round(x, 3) for x in step_ms]},
         "roofline": roofline, "job": job, "cpu_baseline": cpu, "cpu_baseline_copy16": cpu16,
         "cpu_baseline_omp": cpu_omp, "host_nproc": os.cpu_count(), "parity": parity,
-        "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "route_tune": route_tune, "with_win_flags": with_flags,
+        "pcie_inclusive": pcie, "presharded": presharded, "route_ab": route_ab, "route_tune": route_tune, "placement": placement, "with_win_flags": with_flags,
         "gpu_clocks": gpu_clocks,
         "breakdown_ms": {"scan": round(tsum.get("scan_ms", 0) / K, 3),
                          "clock_verify_resolve": round(tsum.get("clock_ms", 0) / K, 3),

@@ -1645,6 +1645,19 @@ struct crdt_ctx {
     bool key_end_valid = false;     // this merge's sorted path reduced its bucket bound (Misc::key_end)
     DBuf<u32x4> p1_rec, p2_rec;        // 16-B partitioned records {lt, rank, val}
     DBuf<uint32_t> p1_kj, p2_kj;       // and their kj words
+    // PlaceTune (crdt_reserve_scratch, CRDT_PLACE_TRIES): the level-1 scatter's time follows where its
+    // destination lands in physical memory (7.6-8.4 ms for the same job on successive
+    // allocations in one process), so an explicit reservation takes several candidate level-1 buffers,
+    // times the scatter on each in the first merges (candidate 0 = p1_*, k >= 1 = pc_*[k]) and keeps the fastest
+    static constexpr int kPlaceMax = 4;
+    DBuf<u32x4> pc_rec[kPlaceMax];
+    DBuf<uint32_t> pc_kj[kPlaceMax];
+    int place_k = 0;                   // candidates under trial (0 / 1: none)
+    int place_trial = 0;               // the next candidate to time
+    int place_best = -1;               // the kept candidate (-1: trials not done)
+    float place_ms[kPlaceMax] = {};    // each candidate's level-1 scatter (ms)
+    bool place_timed = false;          // this call times candidate place_trial
+    hipEvent_t place_ev[2] = {};
     DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
     DBuf<uint64_t> p_plan, p_l1beg;
     DBuf<uint32_t> p_ibase, p_ksu32, p_tseg, p_ibucket;   // resolve items per bucket; part-state / carry u32 columns
@@ -2389,6 +2402,20 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
         // partition buffers, each base shifted by the CRDT_L{1,2}_SHIFT knob (KB; placement A/B runs)
         constexpr size_t kShiftPad = 4u << 20;                      // bytes
+        // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call (swapped back in
+        // place_finish); only while every candidate holds this call's records
+        c->place_timed = false;
+        if (c->place_k > 1 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
+            const int k = c->place_trial;
+            const bool fits = k == 0 ? c->p1_rec.n >= nw + kShiftPad / 16 && c->p1_kj.n >= nw + kShiftPad / 4
+                                     : c->pc_rec[k].n >= nw + kShiftPad / 16 && c->pc_kj[k].n >= nw + kShiftPad / 4;
+            if (fits) {
+                if (k) { std::swap(c->p1_rec, c->pc_rec[k]); std::swap(c->p1_kj, c->pc_kj[k]); }
+                for (hipEvent_t& e : c->place_ev)
+                    if (!e) HIPCHK(hipEventCreate(&e));
+                c->place_timed = true;
+            }
+        }
         HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4, true));
         u32x4* p1r = c->p1_rec.p + (size_t)c->l1_shift_kb * 64;
         uint32_t* p1k = c->p1_kj.p + (size_t)c->l1_shift_kb * 256;
@@ -2422,6 +2449,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const bool ph = c->timing && s0 == 0 && !em;   // phase events: the first window
         if (anchor) ev_record(c, kEvScan);          // (anchored: the keys-only histogram pass and its scans)
         if (ph) ev_record(c, ev_window(1, false));
+        if (c->place_timed) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
         const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
@@ -2471,6 +2499,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         if (ph) ev_record(c, ev_window(1, true));
+        if (c->place_timed) HIPCHK(hipEventRecord(c->place_ev[1], c->stream));
         if (anchor) {
             // the clock phase on the scatter's tile maxima (level-1 tiles of kPTile records): M_j,
             // the recurrence, the exact exception scan of candidate tiles, stop point and canonical
@@ -2919,6 +2948,26 @@ int merge_anchored(crdt_ctx* c, const crdt_batch* b, int64_t wall, const PackFra
     return st;
 }
 
+// After a merge's final synchronisation: the timed candidate's level-1 scatter; after the last trial, the
+// fastest candidate becomes p1 for good and the others are freed.
+void place_finish(crdt_ctx* c, bool ok) {
+    if (!c->place_timed) return;
+    c->place_timed = false;
+    const int k = c->place_trial;
+    if (k) { std::swap(c->p1_rec, c->pc_rec[k]); std::swap(c->p1_kj, c->pc_kj[k]); }   // back in its slot
+    float ms = 0.f;
+    if (!ok || hipEventSynchronize(c->place_ev[1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, c->place_ev[0], c->place_ev[1]) != hipSuccess)
+        return;                                   // (a failed call times nothing: the candidate is tried again)
+    c->place_ms[k] = ms;
+    if (++c->place_trial < c->place_k) return;
+    int b = 0;
+    for (int i = 1; i < c->place_k; ++i) b = c->place_ms[i] < c->place_ms[b] ? i : b;
+    if (b) { std::swap(c->p1_rec, c->pc_rec[b]); std::swap(c->p1_kj, c->pc_kj[b]); }
+    for (int i = 1; i < crdt_ctx::kPlaceMax; ++i) { c->pc_rec[i].release(); c->pc_kj[i].release(); }
+    c->place_best = b;
+}
+
 void collect_timing(crdt_ctx* c) {
     crdt_timing t{};
     if (c->timing) {
@@ -3076,6 +3125,8 @@ void crdt_destroy(crdt_ctx* c) {
     c->d_word.release();
     c->d_ibase.release();
     c->p1_rec.release(); c->p1_kj.release(); c->p2_rec.release(); c->p2_kj.release();
+    for (int i = 0; i < crdt_ctx::kPlaceMax; ++i) { c->pc_rec[i].release(); c->pc_kj[i].release(); }
+    for (hipEvent_t e : c->place_ev) if (e) hipEventDestroy(e);
     c->p_hist.release(); c->p_hist1.release(); c->p_toff.release(); c->p_part.release(); c->p_choff.release();
     c->p_dstart1.release(); c->p_dstart2.release(); c->p_l2map.release();
     c->p_plan.release(); c->p_l1beg.release(); c->h_pplan.release();
@@ -3140,8 +3191,26 @@ int crdt_reserve_scratch(crdt_ctx* c, uint64_t n_records) {
     HIPALLOC(c->p1_kj.ensure(n_records + kShiftPad / 4, true));
     HIPALLOC(c->p2_rec.ensure(n_records + kShiftPad / 16, true));
     HIPALLOC(c->p2_kj.ensure(n_records + kShiftPad / 4, true));
+    // PlaceTune: CRDT_PLACE_TRIES candidate level-1 buffers (default 3; 1 = off), timed in the next merges
+    int tries = 3;
+    if (const char* e = getenv("CRDT_PLACE_TRIES")) tries = std::min(std::max(atoi(e), 1), crdt_ctx::kPlaceMax);
+    if (c->has_comm) tries = 1;                   // (a sharded ctx partitions elsewhere: route_l1, the fold)
+    for (int k = 1; k < tries; ++k) {
+        if (c->pc_rec[k].ensure(n_records + kShiftPad / 16, true) != hipSuccess ||
+            c->pc_kj[k].ensure(n_records + kShiftPad / 4, true) != hipSuccess) {
+            c->pc_rec[k].release();               // no room for more candidates: time those there are
+            c->pc_kj[k].release();
+            tries = k;
+            break;
+        }
+    }
+    c->place_k = tries;
+    c->place_trial = 0;
+    c->place_best = tries > 1 ? -1 : 0;
     return CRDT_OK;
 }
+
+
 
 int crdt_capacity(const crdt_ctx* c, uint64_t* out) {
     if (!c || !out) return CRDT_E_INVALID;
@@ -3410,6 +3479,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
                     ev_record(c, kEvEnd);
                     hipStreamSynchronize(c->stream);
                 }
+                place_finish(c, st >= 0);
                 collect_timing(c);
                 return st;
             }
@@ -3429,6 +3499,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     }
     if (st >= 0 && win_flags && batch->mem == CRDT_MEM_HOST && n)
         HIPCHK(hipMemcpy(win_flags, dflags, n, hipMemcpyDeviceToHost));
+    place_finish(c, st >= 0);
     collect_timing(c);
     return st;
 }
@@ -3479,6 +3550,14 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
     if (c->tune_trial) f |= CRDT_PLAN_ROUTE_TUNED;
     if (c->last_route_l1) f |= (c->last_rl1_pieces & 7u) << CRDT_PLAN_RL1_PIECES_SHIFT;
     *flags = f;
+    return CRDT_OK;
+}
+
+int crdt_place_info(const crdt_ctx* c, int32_t* n, int32_t* kept, float* ms) {
+    if (!c || !n || !kept || !ms) return CRDT_E_INVALID;
+    *n = c->place_k;
+    *kept = c->place_best;
+    for (int i = 0; i < crdt_ctx::kPlaceMax; ++i) ms[i] = i < c->place_k ? c->place_ms[i] : 0.f;
     return CRDT_OK;
 }
 

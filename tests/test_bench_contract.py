@@ -47,6 +47,9 @@ def test_bench_line_contract(gpu_device, path):
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert d["parity"]["equal"] is True and d["parity"]["fields_differing"] == 0
+    pl = d["placement"]                                        # the level-1 placement tuner (sorted path only)
+    assert (pl["kept"] is not None and len(pl["level1_ms"]) == pl["candidates"]) if path == "sorted" \
+        else pl is None or pl["kept"] is None
 
 
 @pytest.mark.gpu

@@ -618,6 +618,43 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
             assert np.array_equal(a, b[rank::2]), rank
 
 
+@pytest.mark.parametrize("tries", ["3", "4", "1"])
+def test_place_tuner_candidates_same_rows(gpu_device, monkeypatch, tries):
+    """The level-1 placement tuner (crdt_reserve_scratch with CRDT_PLACE_TRIES candidate buffers): the
+    first sorted merges run their level-1 scatter on each candidate in turn and the fastest is kept;
+    every call — on every candidate and after the choice — leaves exactly the gather path's rows."""
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    monkeypatch.setenv("CRDT_PLACE_TRIES", tries)
+    K, total, R = 1 << 22, 4_000_000, 128
+    ref, rows = _fanin_reference(K, total, R)
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    loc, own = wl["local"], wl["owned"]
+    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+    t.reserve_scratch(total)
+    t.set_merge_path("sorted")
+    t.set_counts(False)
+    n = int(tries)
+    assert t.place_info()["candidates"] == n and t.place_info()["kept"] == (None if n > 1 else 0)
+    for i in range(n + 2):
+        t.clear_rows(0, wl["capacity"])
+        t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+        t.canonical = wl["c0"]
+        res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                         win_flags=False)
+        info = t.place_info()
+        assert info["kept"] == (None if i + 1 < n else (0 if n == 1 else info["kept"])), (i, info)
+        for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
+            assert res[f] == ref[f], (i, f)
+        for a, b in zip(t.read_rows(np.arange(K, dtype=np.uint32)), rows):
+            assert np.array_equal(a, b), i
+    info = t.place_info()
+    if n > 1:
+        assert info["kept"] in range(n) and all(m > 0 for m in info["level1_ms"]), info
+        assert info["level1_ms"][info["kept"]] == min(info["level1_ms"]), info
+    t.close()
+
+
 @pytest.mark.parametrize("G", [4, 8])
 def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
     """The device-memory collective path — the one RCCL takes: no host synchronisation inside the

@@ -76,12 +76,13 @@ case "${STAGE:-flags}" in
     for i in $(seq 1 ${REPS:-3}); do
       [ -n "${CONTIG_ALT:-}" ] && export CRDT_ALLOC_CONTIG=$(( i % 2 ))
       [ -n "${SHUFFLE_ALT:-}" ] && export CRDT_ALLOC_SHUFFLE=$(( i % 2 ))
+      [ -n "${PLACE_ALT:-}" ] && export CRDT_PLACE_TRIES=$(( i % 2 ? 3 : 1 ))
       timeout -k 10 300 python -u bench.py --steps 6 --warmup 2 --no-cpu --no-census --no-pcie \
         > gpurun_out/${TAG}_spread_$i.json 2> gpurun_out/${TAG}_spread_$i.log
       rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_spread_$i.log; exit $rc; }
       python3 -c "
 import json; d=json.load(open('gpurun_out/${TAG}_spread_$i.json')); g=d.get('gpu_clocks') or {}
-print('run $i contig=${CRDT_ALLOC_CONTIG:-0} shuffle=${CRDT_ALLOC_SHUFFLE:-0}', d['ms_per_step'], 'part1', d['roofline']['dominant_kernel']['phases_ms_per_step']['part1'], 'copy', g.get('copy_GBs'), [(s.get('step_ms'), s.get('part1_ms'), s.get('sclk_mhz'), s.get('power_w')) for s in g.get('per_step', [])])"
+print('run $i contig=${CRDT_ALLOC_CONTIG:-0} shuffle=${CRDT_ALLOC_SHUFFLE:-0} place=${CRDT_PLACE_TRIES:-3}', d.get('placement'), d['ms_per_step'], 'part1', d['roofline']['dominant_kernel']['phases_ms_per_step']['part1'], 'copy', g.get('copy_GBs'), [(s.get('step_ms'), s.get('part1_ms'), s.get('sclk_mhz'), s.get('power_w')) for s in g.get('per_step', [])])"
     done ;;
   misc)
     # the wide clock frame with win flags; the anchored form's PMC traffic (item 3);
