@@ -2404,7 +2404,6 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         constexpr size_t kShiftPad = 4u << 20;                      // bytes
         // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call (swapped back in
         // place_finish); only while every candidate holds this call's records
-        c->place_timed = false;
         if (c->place_k > 1 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
             const int k = c->place_trial;
             const bool fits = k == 0 ? c->p1_rec.n >= nw + kShiftPad / 16 && c->p1_kj.n >= nw + kShiftPad / 4
@@ -2449,7 +2448,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const bool ph = c->timing && s0 == 0 && !em;   // phase events: the first window
         if (anchor) ev_record(c, kEvScan);          // (anchored: the keys-only histogram pass and its scans)
         if (ph) ev_record(c, ev_window(1, false));
-        if (c->place_timed) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));
+        if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));   // (the first window)
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
         const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
@@ -2499,7 +2498,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
                 p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
         if (ph) ev_record(c, ev_window(1, true));
-        if (c->place_timed) HIPCHK(hipEventRecord(c->place_ev[1], c->stream));
+        if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[1], c->stream));
         if (anchor) {
             // the clock phase on the scatter's tile maxima (level-1 tiles of kPTile records): M_j,
             // the recurrence, the exact exception scan of candidate tiles, stop point and canonical
@@ -3429,6 +3428,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         ~HwUpdate() { c->hw = std::max(c->hw, c->hw_next); }
     } hw_update{c};
     if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
+    c->place_timed = false;                                  // (set by this call's first sorted window)
     // Host batches are staged once; every phase then sees device columns.
     crdt_batch dev = *batch;
     uint8_t* dflags = win_flags;

@@ -618,15 +618,17 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
             assert np.array_equal(a, b[rank::2]), rank
 
 
-@pytest.mark.parametrize("tries", ["3", "4", "1"])
-def test_place_tuner_candidates_same_rows(gpu_device, monkeypatch, tries):
+@pytest.mark.parametrize("tries,R", [("3", 128), ("4", 128), ("1", 128), ("3", 2048)])
+def test_place_tuner_candidates_same_rows(gpu_device, monkeypatch, tries, R):
     """The level-1 placement tuner (crdt_reserve_scratch with CRDT_PLACE_TRIES candidate buffers): the
     first sorted merges run their level-1 scatter on each candidate in turn and the fastest is kept;
-    every call — on every candidate and after the choice — leaves exactly the gather path's rows."""
+    every call — on every candidate and after the choice — leaves exactly the gather path's rows.
+    (2048 changesets: more than the packed key's changeset window, so a call partitions in several
+    windows, every one on the candidate under trial.)"""
     from crdt_amd import DeviceTable
     from crdt_amd.workload import gen_fanin
     monkeypatch.setenv("CRDT_PLACE_TRIES", tries)
-    K, total, R = 1 << 22, 4_000_000, 128
+    K, total = 1 << 22, 4_000_000
     ref, rows = _fanin_reference(K, total, R)
     wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
     loc, own = wl["local"], wl["owned"]
