@@ -2402,18 +2402,19 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
         // partition buffers, each base shifted by the CRDT_L{1,2}_SHIFT knob (KB; placement A/B runs)
         constexpr size_t kShiftPad = 4u << 20;                      // bytes
-        // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call (swapped back in
-        // place_finish); only while every candidate holds this call's records
+        // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call, every window
+        // of it (swapped back in place_finish)
         if (c->place_k > 1 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
             const int k = c->place_trial;
-            const bool fits = k == 0 ? c->p1_rec.n >= nw + kShiftPad / 16 && c->p1_kj.n >= nw + kShiftPad / 4
-                                     : c->pc_rec[k].n >= nw + kShiftPad / 16 && c->pc_kj[k].n >= nw + kShiftPad / 4;
-            if (fits) {
-                if (k) { std::swap(c->p1_rec, c->pc_rec[k]); std::swap(c->p1_kj, c->pc_kj[k]); }
-                for (hipEvent_t& e : c->place_ev)
-                    if (!e) HIPCHK(hipEventCreate(&e));
-                c->place_timed = true;
+            if (k) {                                  // (grown like p1 itself when this call holds more records)
+                HIPALLOC(c->pc_rec[k].ensure(nw + kShiftPad / 16, true));
+                HIPALLOC(c->pc_kj[k].ensure(nw + kShiftPad / 4, true));
+                std::swap(c->p1_rec, c->pc_rec[k]);
+                std::swap(c->p1_kj, c->pc_kj[k]);
             }
+            for (hipEvent_t& e : c->place_ev)
+                if (!e) HIPCHK(hipEventCreate(&e));
+            c->place_timed = true;
         }
         HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4, true));
         u32x4* p1r = c->p1_rec.p + (size_t)c->l1_shift_kb * 64;
