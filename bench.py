@@ -351,14 +351,14 @@ def main():
     # the level-1 scatter on each in the first merges and keeps the fastest — also before the warmup
     placement = None
     if world == 1 and table.place_info()["candidates"] > 1:
-        for _ in range(6):
+        for _ in range(8):                               # (a warm-up merge, then one per candidate)
             before = table.place_info()
             if before["kept"] is not None:
                 break
             reset()
             step()
-            if table.place_info() == before:            # (this path does not partition: nothing to time)
-                break
+            if table.place_info()["merges_used"] == before["merges_used"]:
+                break                                    # (this path does not partition: nothing to time)
         placement = table.place_info()
         log(f"placement tuner: {placement}")
     for _ in range(args.warmup):

@@ -116,7 +116,7 @@ SIGNATURES = {
     "crdt_set_row_bytes": (_INT, [_P, _U32]),
     "crdt_last_plan": (_INT, [_P, _P]),
     "crdt_route_tune_info": (_INT, [_P, _P, _P]),
-    "crdt_place_info": (_INT, [_P, _P, _P, _P]),
+    "crdt_place_info": (_INT, [_P, _P, _P, _P, _P]),
     "crdt_last_path": (_INT, [_P, _P]),
     "crdt_set_timing": (_INT, [_P, _INT]),
     "crdt_get_timing": (_INT, [_P, _P]),

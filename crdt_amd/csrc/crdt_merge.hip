@@ -1653,10 +1653,11 @@ struct crdt_ctx {
     DBuf<u32x4> pc_rec[kPlaceMax];
     DBuf<uint32_t> pc_kj[kPlaceMax];
     int place_k = 0;                   // candidates under trial (0 / 1: none)
-    int place_trial = 0;               // the next candidate to time
+    int place_trial = 0;               // the next candidate to time (-1: the warm-up merge comes first)
     int place_best = -1;               // the kept candidate (-1: trials not done)
     float place_ms[kPlaceMax] = {};    // each candidate's level-1 scatter (ms)
     bool place_timed = false;          // this call times candidate place_trial
+    bool place_warm = false;           // this call is the untimed warm-up (the kernels' first launch loads them)
     hipEvent_t place_ev[2] = {};
     DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
     DBuf<uint64_t> p_plan, p_l1beg;
@@ -2404,7 +2405,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         constexpr size_t kShiftPad = 4u << 20;                      // bytes
         // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call, every window
         // of it (swapped back in place_finish)
-        if (c->place_k > 1 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
+        if (c->place_k > 1 && c->place_trial < 0 && !c->has_comm && s0 == 0) c->place_warm = true;
+        if (c->place_k > 1 && c->place_trial >= 0 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
             const int k = c->place_trial;
             if (k) {                                  // (grown like p1 itself when this call holds more records)
                 HIPALLOC(c->pc_rec[k].ensure(nw + kShiftPad / 16, true));
@@ -2951,6 +2953,11 @@ int merge_anchored(crdt_ctx* c, const crdt_batch* b, int64_t wall, const PackFra
 // After a merge's final synchronisation: the timed candidate's level-1 scatter; after the last trial, the
 // fastest candidate becomes p1 for good and the others are freed.
 void place_finish(crdt_ctx* c, bool ok) {
+    if (c->place_warm) {
+        c->place_warm = false;
+        if (ok) c->place_trial = 0;
+        return;
+    }
     if (!c->place_timed) return;
     c->place_timed = false;
     const int k = c->place_trial;
@@ -3205,7 +3212,7 @@ int crdt_reserve_scratch(crdt_ctx* c, uint64_t n_records) {
         }
     }
     c->place_k = tries;
-    c->place_trial = 0;
+    c->place_trial = tries > 1 ? -1 : 0;
     c->place_best = tries > 1 ? -1 : 0;
     return CRDT_OK;
 }
@@ -3429,7 +3436,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         ~HwUpdate() { c->hw = std::max(c->hw, c->hw_next); }
     } hw_update{c};
     if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
-    c->place_timed = false;                                  // (set by this call's first sorted window)
+    c->place_timed = c->place_warm = false;                  // (set by this call's first sorted window)
     // Host batches are staged once; every phase then sees device columns.
     crdt_batch dev = *batch;
     uint8_t* dflags = win_flags;
@@ -3554,10 +3561,11 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
     return CRDT_OK;
 }
 
-int crdt_place_info(const crdt_ctx* c, int32_t* n, int32_t* kept, float* ms) {
-    if (!c || !n || !kept || !ms) return CRDT_E_INVALID;
+int crdt_place_info(const crdt_ctx* c, int32_t* n, int32_t* kept, int32_t* done, float* ms) {
+    if (!c || !n || !kept || !done || !ms) return CRDT_E_INVALID;
     *n = c->place_k;
     *kept = c->place_best;
+    *done = c->place_k > 1 ? c->place_trial + 1 : 0;
     for (int i = 0; i < crdt_ctx::kPlaceMax; ++i) ms[i] = i < c->place_k ? c->place_ms[i] : 0.f;
     return CRDT_OK;
 }

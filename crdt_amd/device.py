@@ -324,11 +324,13 @@ class DeviceTable:
 
     def place_info(self) -> dict:
         """crdt_place_info: the level-1 placement tuner ({'candidates': n, 'kept': index or None while the
-        trials run, 'level1_ms': each candidate's timed level-1 scatter})."""
-        n, kept = ctypes.c_int32(0), ctypes.c_int32(0)
+        trials run, 'merges_used': the warm-up + one merge per candidate so far, 'level1_ms': each candidate's
+        timed level-1 scatter})."""
+        n, kept, done = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
         ms = (ctypes.c_float * 4)()
-        self._check(self._lib.crdt_place_info(self._ctx, ctypes.byref(n), ctypes.byref(kept), ms), "crdt_place_info")
-        return {"candidates": n.value, "kept": kept.value if kept.value >= 0 else None,
+        self._check(self._lib.crdt_place_info(self._ctx, ctypes.byref(n), ctypes.byref(kept), ctypes.byref(done), ms),
+                    "crdt_place_info")
+        return {"candidates": n.value, "kept": kept.value if kept.value >= 0 else None, "merges_used": done.value,
                 "level1_ms": [round(float(m), 3) for m in ms[:max(n.value, 0)]]}
 
     TUNE_WAYS = ("route_l1", "combine", "route_l1_4", "route_l1_1")
