@@ -351,7 +351,7 @@ def main():
     # the level-1 scatter on each in the first merges and keeps the fastest — also before the warmup
     placement = None
     if world == 1 and table.place_info()["candidates"] > 1:
-        for _ in range(8):                               # (a warm-up merge, then one per candidate)
+        for _ in range(10):                              # (a warm-up merge, then two per candidate)
             before = table.place_info()
             if before["kept"] is not None:
                 break

@@ -1653,9 +1653,10 @@ struct crdt_ctx {
     DBuf<u32x4> pc_rec[kPlaceMax];
     DBuf<uint32_t> pc_kj[kPlaceMax];
     int place_k = 0;                   // candidates under trial (0 / 1: none)
-    int place_trial = 0;               // the next candidate to time (-1: the warm-up merge comes first)
+    int place_trial = 0;               // trials done (-1: the warm-up merge comes first); candidate = trial % k,
+                                       // two rounds (the clocks still settle over the first merges)
     int place_best = -1;               // the kept candidate (-1: trials not done)
-    float place_ms[kPlaceMax] = {};    // each candidate's level-1 scatter (ms)
+    float place_ms[kPlaceMax] = {};    // each candidate's level-1 scatter (ms; the faster of its two trials)
     bool place_timed = false;          // this call times candidate place_trial
     bool place_warm = false;           // this call is the untimed warm-up (the kernels' first launch loads them)
     hipEvent_t place_ev[2] = {};
@@ -2406,8 +2407,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call, every window
         // of it (swapped back in place_finish)
         if (c->place_k > 1 && c->place_trial < 0 && !c->has_comm && s0 == 0) c->place_warm = true;
-        if (c->place_k > 1 && c->place_trial >= 0 && c->place_trial < c->place_k && !c->has_comm && s0 == 0) {
-            const int k = c->place_trial;
+        if (c->place_k > 1 && c->place_trial >= 0 && c->place_trial < 2 * c->place_k && !c->has_comm && s0 == 0) {
+            const int k = c->place_trial % c->place_k;
             if (k) {                                  // (grown like p1 itself when this call holds more records)
                 HIPALLOC(c->pc_rec[k].ensure(nw + kShiftPad / 16, true));
                 HIPALLOC(c->pc_kj[k].ensure(nw + kShiftPad / 4, true));
@@ -2960,14 +2961,14 @@ void place_finish(crdt_ctx* c, bool ok) {
     }
     if (!c->place_timed) return;
     c->place_timed = false;
-    const int k = c->place_trial;
+    const int k = c->place_trial % c->place_k;
     if (k) { std::swap(c->p1_rec, c->pc_rec[k]); std::swap(c->p1_kj, c->pc_kj[k]); }   // back in its slot
     float ms = 0.f;
     if (!ok || hipEventSynchronize(c->place_ev[1]) != hipSuccess ||
         hipEventElapsedTime(&ms, c->place_ev[0], c->place_ev[1]) != hipSuccess)
         return;                                   // (a failed call times nothing: the candidate is tried again)
-    c->place_ms[k] = ms;
-    if (++c->place_trial < c->place_k) return;
+    c->place_ms[k] = c->place_trial < c->place_k ? ms : std::min(c->place_ms[k], ms);
+    if (++c->place_trial < 2 * c->place_k) return;
     int b = 0;
     for (int i = 1; i < c->place_k; ++i) b = c->place_ms[i] < c->place_ms[b] ? i : b;
     if (b) { std::swap(c->p1_rec, c->pc_rec[b]); std::swap(c->p1_kj, c->pc_kj[b]); }

@@ -324,8 +324,8 @@ class DeviceTable:
 
     def place_info(self) -> dict:
         """crdt_place_info: the level-1 placement tuner ({'candidates': n, 'kept': index or None while the
-        trials run, 'merges_used': the warm-up + one merge per candidate so far, 'level1_ms': each candidate's
-        timed level-1 scatter})."""
+        trials run, 'merges_used': the warm-up + two merges per candidate so far, 'level1_ms': each candidate's
+        timed level-1 scatter, the faster of its two trials})."""
         n, kept, done = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
         ms = (ctypes.c_float * 4)()
         self._check(self._lib.crdt_place_info(self._ctx, ctypes.byref(n), ctypes.byref(kept), ctypes.byref(done), ms),

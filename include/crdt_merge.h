@@ -311,10 +311,11 @@ int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [4] 
 
 /* The level-1 scatter's placement tuner (crdt_merge.hip, PlaceTune; CRDT_PLACE_TRIES, default 3, 1 = off):
  * crdt_reserve_scratch on a single-GPU ctx takes that many candidate level-1 partition buffers; the next
- * sorted-path merges — after one untimed warm-up merge — time the level-1 scatter on each in turn and keep
- * the fastest (the scatter's time follows where its destination lies in physical memory).
- * *n: candidates (0 / 1: no trials); *kept: the kept one (-1 while the trials run); *done: merges the
- * tuner has used (the warm-up, then one per candidate); ms[0 .. 3]: each candidate's level-1 scatter. */
+ * sorted-path merges — after one untimed warm-up merge — time the level-1 scatter on each in turn, two
+ * rounds, and keep the fastest (the scatter's time follows where its destination lies in physical memory;
+ * DESIGN.md §6).  *n: candidates (0 / 1: no trials); *kept: the kept one (-1 while the trials run); *done:
+ * merges the tuner has used (the warm-up, then two per candidate); ms[0 .. 3]: each candidate's level-1
+ * scatter (the faster of its two trials). */
 int crdt_place_info(const crdt_ctx* ctx, int32_t* n, int32_t* kept, int32_t* done, float* ms /* [4] */);
 
 /* ---- measurement ---------------------------------------------------------- */

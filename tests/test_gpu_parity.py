@@ -638,15 +638,15 @@ def test_place_tuner_candidates_same_rows(gpu_device, monkeypatch, tries, R):
     t.set_counts(False)
     n = int(tries)
     assert t.place_info()["candidates"] == n and t.place_info()["kept"] == (None if n > 1 else 0)
-    for i in range(n + 3):                                    # (the warm-up merge, then one per candidate)
+    for i in range(2 * n + 2):                                # (the warm-up merge, then two per candidate)
         t.clear_rows(0, wl["capacity"])
         t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
         t.canonical = wl["c0"]
         res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
                          win_flags=False)
         info = t.place_info()
-        assert info["kept"] == (0 if n == 1 else None if i < n else info["kept"]), (i, info)
-        assert info["merges_used"] == (0 if n == 1 else min(i + 1, n + 1)), (i, info)
+        assert info["kept"] == (0 if n == 1 else None if i < 2 * n else info["kept"]), (i, info)
+        assert info["merges_used"] == (0 if n == 1 else min(i + 1, 2 * n + 1)), (i, info)
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
             assert res[f] == ref[f], (i, f)
         for a, b in zip(t.read_rows(np.arange(K, dtype=np.uint32)), rows):
