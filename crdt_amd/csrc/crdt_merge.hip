@@ -1679,6 +1679,7 @@ struct crdt_ctx {
     uint32_t l1_shift_kb = 0, l2_shift_kb = 0;   // CRDT_L1_SHIFT / CRDT_L2_SHIFT (KB, < 4096)          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
+    uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (A/B; 0 = kPTile)
     bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
     // level-1 histogram counted by the scan (k_scan<.., kHist>) for the sorted path of this plan
@@ -2376,13 +2377,16 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         uint32_t* h_sj = reinterpret_cast<uint32_t*>(c->h_pplan.p + 2 * (size_t)nseg);
         uint32_t* tb = h_sj + nseg;
         uint32_t nt1 = 0;
+        // level-1 tile (CRDT_L1_TILE, A/B): kPTile, whose level-1 histogram the scan counts; another size
+        // (a multiple of 1024) takes the histogram pass
+        const uint32_t l1t = (c->l1_tile && !anchor) ? c->l1_tile : (uint32_t)kPTile;
         for (uint32_t s = 0; s <= nseg; ++s) {
             tb[s] = nt1;
             if (s < nseg) {
                 h_beg[s] = sg.beg[s0 + s];
                 h_end[s] = sg.end[s0 + s];
                 h_sj[s] = sg.j[s0 + s];
-                nt1 += (uint32_t)((h_end[s] - h_beg[s] + kPTile - 1) / kPTile);
+                nt1 += (uint32_t)((h_end[s] - h_beg[s] + l1t - 1) / l1t);
             }
         }
         const uint32_t nc1 = (nt1 + kChunkTiles - 1) / kChunkTiles;
@@ -2430,7 +2434,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         const uint32_t* d_tb1 = d_sj + nseg;
         HIPALLOC(c->p_tseg.ensure(ntm));
         k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1, c->p_tseg.p);
-        const TileMap tm1{d_beg, d_end, d_tb1, c->p_tseg.p, d_sj, nseg, (uint32_t)kPTile};
+        const TileMap tm1{d_beg, d_end, d_tb1, c->p_tseg.p, d_sj, nseg, l1t};
         const ScanMap sm1{reinterpret_cast<const uint32_t*>(c->p_plan.p + tail),
                           reinterpret_cast<const uint32_t*>(c->p_plan.p + tail + 1), c->p_plan.p + tail + 2, 1};
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
@@ -3059,6 +3063,8 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
     if (const char* e = getenv("CRDT_FBACK_CHK")) c->fback_chk = atoi(e) == 4 ? 4 : atoi(e) == 0 ? 0 : 6;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_L1_TILE"))
+        c->l1_tile = std::min<uint32_t>((uint32_t)std::max(atoi(e), 0) / 1024u * 1024u, (uint32_t)kPTile);
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
     if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
     if (const char* e = getenv("CRDT_L2_SHIFT")) c->l2_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
