@@ -225,7 +225,7 @@ __host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ul
 // keys are read with lt and counted per level-1 partition tile (kHistSub scan tiles, never
 // straddling a changeset) into hist[ptb[j] + u][256] — what k_part_hist<true> would write with
 // every changeset applied (tiles of changesets >= stop are zeroed once stop is known).
-constexpr uint32_t kHistSub = 8;                 // scan tiles per level-1 partition tile
+constexpr uint32_t kHistSub = 7;                 // scan tiles per level-1 partition tile
 
 // The level-1 digit of a key id.  One ctx: (k >> shift) & 255 over the ids k < cap.  The routed
 // partition of a sharded order-free merge (comm_path.inc, route_l1) partitions GLOBAL key ids of G = 2^gsh
