@@ -8,6 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu --no-census --no-pcie"}
 MERGES=${MERGES:-3}                 # merges the command runs (warmup + steps)
+export CRDT_PLACE_TRIES=1           # (no placement-trial merges: the bytes of a step do not depend on them)
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py $ARGS > gpurun_out/pmc_fetch.log 2>&1
 rc=$?; echo "[fetch] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_fetch.log; exit $rc; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py $ARGS > gpurun_out/pmc_write.log 2>&1
