@@ -128,7 +128,9 @@ void crdt_destroy(crdt_ctx* ctx);
 int crdt_reserve(crdt_ctx* ctx, uint64_t capacity);          /* grow; new rows absent */
 /* Pre-size the sorted path's partition scratch for merges of up to n_records applied records
  * (two partitioned copies, <= 40 B per record), so the first large merge allocates nothing and the
- * buffers are placed while device memory is still unfragmented.  Optional. */
+ * buffers are placed while device memory is still unfragmented.  On a single-GPU ctx it also takes the
+ * placement tuner's candidate level-1 buffers (CRDT_PLACE_TRIES - 1 more, <= 20 B per record each; freed
+ * once the first merges have timed them: crdt_place_info).  Optional. */
 int crdt_reserve_scratch(crdt_ctx* ctx, uint64_t n_records);
 /* Row size of the device table: 24 (default) or 32 bytes; the rows are copied over.  24-B rows move
  * 25 % fewer bytes in the sorted path's coalesced passes (many-changeset fan-ins); 32-B rows make
