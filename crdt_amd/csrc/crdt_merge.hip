@@ -222,10 +222,14 @@ __host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ul
 // (lt and rank bounds) into misc->fr_*, one set of atomics per workgroup and tile, only where
 // it moves a bound (a stale read of a bound never makes a needed atomic look useless)
 // kHist (the sorted path's level-1 histogram fused into the scan, single ctx, one window): the
-// keys are read with lt and counted per level-1 partition tile (kHistSub scan tiles, never
-// straddling a changeset) into hist[ptb[j] + u][256] — what k_part_hist<true> would write with
-// every changeset applied (tiles of changesets >= stop are zeroed once stop is known).
-constexpr uint32_t kHistSub = 7;                 // scan tiles per level-1 partition tile
+// keys are read with lt and counted per level-1 partition tile (never straddling a changeset) into
+// hist[ptb[j] + u][256] — what k_part_hist<true> would write with every changeset applied (tiles of
+// changesets >= stop are zeroed once stop is known).  A workgroup takes kHistSub scan tiles = kHistPer
+// level-1 tiles per step: a level-1 tile is 3.5 scan tiles, its boundary in the middle of every seventh
+// ... fourth scan tile, where a thread's record groups split cleanly (whole 1024- / 256-record groups).
+constexpr uint32_t kHistSub = 7;                 // scan tiles per workgroup step of the fused histogram
+constexpr uint32_t kHistPer = 2;                 // ... level-1 partition tiles it counts
+constexpr uint32_t kHistTile = kHistSub * kTile / kHistPer;   // = kPTile (sorted_path.inc checks)
 
 // The level-1 digit of a key id.  One ctx: (k >> shift) & 255 over the ids k < cap.  The routed
 // partition of a sharded order-free merge (comm_path.inc, route_l1) partitions GLOBAL key ids of G = 2^gsh
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
     __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
-    __shared__ uint32_t s_h[kHist ? 256 : 1];
+    __shared__ uint32_t s_h[kHist ? 256 * kHistPer : 1];
     static_assert(!kHist || kScanThreads == 256, "one histogram bin per thread");
     const uint32_t j = jbase + blockIdx.y;
     const uint64_t beg = offs[j], end = offs[j + 1];
@@ -272,7 +276,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     constexpr uint32_t kStep = kHist ? kHistSub : 1u;
     for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
       if (kHist) {
-        s_h[threadIdx.x] = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < kHistPer; ++h) s_h[h * 256 + threadIdx.x] = 0;
         __syncthreads();
       }
       const uint32_t te = std::min<uint32_t>(u * kStep + kStep, nt);
@@ -319,10 +324,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             m = imax(m, v[q]);
         }
         if (kHist) {
+            const uint32_t tb = (t - u * kStep) * (uint32_t)kTile;      // this scan tile inside the step
 #pragma unroll
             for (int q = 0; q < kScanItems; ++q) {
                 const uint32_t k = kk[kHist ? q : 0];
-                digit_count(s_h, km_digit(sh.km, k, sh.shift), (k >> sh.km.gsh) < sh.cap, lane);
+                // the record's level-1 tile of the step: the same for the whole workgroup at a given q
+                // (its group / stride base decides; the thread offset stays below the 1024 / 256 grain)
+                const uint32_t gb = kVec ? (uint32_t)(q >> 2) * (4u * kScanThreads) : (uint32_t)q * kScanThreads;
+                const uint32_t h = (tb + gb) / kHistTile;
+                digit_count(s_h + 256u * (h < kHistPer ? h : kHistPer - 1), km_digit(sh.km, k, sh.shift),
+                            (k >> sh.km.gsh) < sh.cap, lane);
             }
         }
         // rank / millis matter only for records above C0 (the only ones recv() can raise on)
@@ -389,7 +400,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         }
         __syncthreads();
       }
-      if (kHist) sh.hist[(uint64_t)(sh.ptb[j] + u) * 256 + threadIdx.x] = s_h[threadIdx.x];
+      if (kHist) {
+        const uint32_t np = sh.ptb[j + 1] - sh.ptb[j];                  // the changeset's level-1 tiles
+#pragma unroll
+        for (uint32_t h = 0; h < kHistPer; ++h)
+            if (u * kHistPer + h < np)
+                sh.hist[(uint64_t)(sh.ptb[j] + u * kHistPer + h) * 256 + threadIdx.x] = s_h[h * 256 + threadIdx.x];
+      }
     }
 }
 
@@ -1882,7 +1899,7 @@ int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t*
             const uint64_t nj = b->offsets[j + 1] - b->offsets[j];
             const uint64_t tj = (nj + kTile - 1) / kTile;
             tiles += tj;
-            ptiles += (tj + kHistSub - 1) / kHistSub;
+            ptiles += (nj + kPTile - 1) / kPTile;
             mt = std::max<uint32_t>(mt, (uint32_t)tj);
         }
     }
