@@ -224,12 +224,11 @@ __host__ __device__ inline uint64_t ord64(int64_t x) { return (uint64_t)x ^ (1ul
 // kHist (the sorted path's level-1 histogram fused into the scan, single ctx, one window): the
 // keys are read with lt and counted per level-1 partition tile (never straddling a changeset) into
 // hist[ptb[j] + u][256] — what k_part_hist<true> would write with every changeset applied (tiles of
-// changesets >= stop are zeroed once stop is known).  A workgroup takes kHistSub scan tiles = kHistPer
-// level-1 tiles per step: a level-1 tile is 3.5 scan tiles, its boundary in the middle of every seventh
-// ... fourth scan tile, where a thread's record groups split cleanly (whole 1024- / 256-record groups).
+// changesets >= stop are zeroed once stop is known).  A workgroup takes kHistSub scan tiles per step:
+// one level-1 tile of 28672 records, or two of 14336 (ScanHist::htile) — then the boundary falls in the
+// middle of the step's fourth scan tile, where a thread's record groups split cleanly (whole 1024- /
+// 256-record groups, so every record of one load instruction counts into the same histogram).
 constexpr uint32_t kHistSub = 7;                 // scan tiles per workgroup step of the fused histogram
-constexpr uint32_t kHistPer = 2;                 // ... level-1 partition tiles it counts
-constexpr uint32_t kHistTile = kHistSub * kTile / kHistPer;   // = kPTile (sorted_path.inc checks)
 
 // The level-1 digit of a key id.  One ctx: (k >> shift) & 255 over the ids k < cap.  The routed
 // partition of a sharded order-free merge (comm_path.inc, route_l1) partitions GLOBAL key ids of G = 2^gsh
@@ -251,6 +250,7 @@ struct ScanHist {
     uint32_t shift;
     uint32_t* hist;
     KeyMap km{0u, 8u};
+    uint32_t htile = kHistSub * kTile;      // level-1 tile (records): the step's 28672, or 14336 (two per step)
 };
 
 // kVec: a thread's records are 4 groups of 4 consecutive ones (lt read with two 16-B loads per
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
     __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
-    __shared__ uint32_t s_h[kHist ? 256 * kHistPer : 1];
+    __shared__ uint32_t s_h[kHist ? 512 : 1];
     static_assert(!kHist || kScanThreads == 256, "one histogram bin per thread");
     const uint32_t j = jbase + blockIdx.y;
     const uint64_t beg = offs[j], end = offs[j + 1];
@@ -276,8 +276,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     constexpr uint32_t kStep = kHist ? kHistSub : 1u;
     for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
       if (kHist) {
-#pragma unroll
-        for (uint32_t h = 0; h < kHistPer; ++h) s_h[h * 256 + threadIdx.x] = 0;
+        s_h[threadIdx.x] = 0;
+        s_h[256 + threadIdx.x] = 0;
         __syncthreads();
       }
       const uint32_t te = std::min<uint32_t>(u * kStep + kStep, nt);
@@ -331,8 +331,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                 // the record's level-1 tile of the step: the same for the whole workgroup at a given q
                 // (its group / stride base decides; the thread offset stays below the 1024 / 256 grain)
                 const uint32_t gb = kVec ? (uint32_t)(q >> 2) * (4u * kScanThreads) : (uint32_t)q * kScanThreads;
-                const uint32_t h = (tb + gb) / kHistTile;
-                digit_count(s_h + 256u * (h < kHistPer ? h : kHistPer - 1), km_digit(sh.km, k, sh.shift),
+                digit_count(s_h + (tb + gb >= sh.htile ? 256u : 0u), km_digit(sh.km, k, sh.shift),
                             (k >> sh.km.gsh) < sh.cap, lane);
             }
         }
@@ -402,10 +401,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
       }
       if (kHist) {
         const uint32_t np = sh.ptb[j + 1] - sh.ptb[j];                  // the changeset's level-1 tiles
-#pragma unroll
-        for (uint32_t h = 0; h < kHistPer; ++h)
-            if (u * kHistPer + h < np)
-                sh.hist[(uint64_t)(sh.ptb[j] + u * kHistPer + h) * 256 + threadIdx.x] = s_h[h * 256 + threadIdx.x];
+        const uint32_t per = sh.htile < kHistSub * kTile ? 2u : 1u;
+        for (uint32_t h = 0; h < per; ++h)
+            if (u * per + h < np)
+                sh.hist[(uint64_t)(sh.ptb[j] + u * per + h) * 256 + threadIdx.x] = s_h[h * 256 + threadIdx.x];
       }
     }
 }
@@ -1696,7 +1695,7 @@ struct crdt_ctx {
     uint32_t l1_shift_kb = 0, l2_shift_kb = 0;   // CRDT_L1_SHIFT / CRDT_L2_SHIFT (KB, < 4096)          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
-    uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (A/B; 0 = kPTile)
+    uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (0 = the default, kL1TileDefault)
     bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
     // level-1 histogram counted by the scan (k_scan<.., kHist>) for the sorted path of this plan
@@ -1796,6 +1795,15 @@ struct crdt_ctx {
     HBuf<uint8_t> h_stage;                                // CRDT_MEM_HOST backends
     HBuf<long long> h_sum;                                // reduced counts / error / uncounted
 };
+
+// The level-1 partition tile (records).  The default and 14336 / 28672 are tiles the scan's fused histogram
+// counts (one or two per seven scan tiles) and the plan's ptb is laid out in; any other CRDT_L1_TILE (a
+// multiple of 1024, an A/B) partitions in its own tiles with the separate histogram pass.
+constexpr uint32_t kL1TileDefault = 28672;
+inline uint32_t l1_plan_tile(const crdt_ctx* c) {
+    return c->l1_tile == 14336u || c->l1_tile == 28672u ? c->l1_tile : kL1TileDefault;
+}
+
 
 namespace {
 
@@ -1899,7 +1907,7 @@ int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t*
             const uint64_t nj = b->offsets[j + 1] - b->offsets[j];
             const uint64_t tj = (nj + kTile - 1) / kTile;
             tiles += tj;
-            ptiles += (nj + kPTile - 1) / kPTile;
+            ptiles += (nj + l1_plan_tile(c) - 1) / l1_plan_tile(c);
             mt = std::max<uint32_t>(mt, (uint32_t)tj);
         }
     }
@@ -1990,6 +1998,9 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         c->hist1_shift = rhist || c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
     }
     ScanHist shr{home->key_id, c->d_ptb, c->cap, 20u, c->p_hist1.p};
+    shr.htile = l1_plan_tile(c);
+    ScanHist shist{home->key_id, c->d_ptb, c->cap, c->hist1_shift, c->p_hist1.p};
+    shist.htile = l1_plan_tile(c);
     if (rhist) shr.km = *route_km;
     if (tiles) {
         // grid.x: tiles of one changeset strided over at most ~64K blocks in total
@@ -2006,12 +2017,11 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
                 k_scan<false, true, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
-                    ScanHist{home->key_id, c->d_ptb, c->cap, c->hist1_shift, c->p_hist1.p});
+                    shist);
             else if (hist)
                 k_scan<false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
-                    ScanHist{home->key_id, c->d_ptb, c->cap, c->hist1_shift, c->p_hist1.p});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shist);
             else if (c->frame_lt_only)                    // lt frame only: ranks loaded lazily as usual
                 k_scan<false, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
@@ -2396,7 +2406,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         uint32_t nt1 = 0;
         // level-1 tile (CRDT_L1_TILE, A/B): kPTile, whose level-1 histogram the scan counts; another size
         // (a multiple of 1024) takes the histogram pass
-        const uint32_t l1t = (c->l1_tile && !anchor) ? c->l1_tile : (uint32_t)kPTile;
+        const uint32_t l1t = anchor ? l1_plan_tile(c) : c->l1_tile ? c->l1_tile : kL1TileDefault;
         for (uint32_t s = 0; s <= nseg; ++s) {
             tb[s] = nt1;
             if (s < nseg) {
@@ -2533,7 +2543,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             k_verify<false><<<kVerifyBlocks, 64, 0, c->stream>>>(
                 cols.lt, cols.rank, nullptr, c->d_offs, c->d_ptb, R, c->d_T.p, c->d_Cprev.p, wall, c->local_rank,
                 c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p, c->d_candms.p, nullptr,
-                nullptr, c->d_event.p, 0, nullptr, nullptr, (uint32_t)kPTile);
+                nullptr, c->d_event.p, 0, nullptr, nullptr, l1t);
             k_resolve_local<<<1, 256, 0, c->stream>>>(c->d_misc, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
                                                       c->d_candms.p, c->d_event.p);
             k_resolve<<<1, 64, 0, c->stream>>>(c->d_event.p, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
