@@ -1695,7 +1695,8 @@ struct crdt_ctx {
     uint32_t l1_shift_kb = 0, l2_shift_kb = 0;   // CRDT_L1_SHIFT / CRDT_L2_SHIFT (KB, < 4096)          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
-    uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (0 = the default, kL1TileDefault)
+    uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (0 = chosen per plan: l1_choose)
+    uint32_t plan_l1_tile = 28672;  // the level-1 tile of the current plan (ptb, the scan's fused histogram)
     bool last_hist1_fused = false;
     bool frame_lt_only = false;     // this plan's frame: lt from the scan, ranks from rank_bound
     // level-1 histogram counted by the scan (k_scan<.., kHist>) for the sorted path of this plan
@@ -1799,10 +1800,15 @@ struct crdt_ctx {
 // The level-1 partition tile (records).  The default and 14336 / 28672 are tiles the scan's fused histogram
 // counts (one or two per seven scan tiles) and the plan's ptb is laid out in; any other CRDT_L1_TILE (a
 // multiple of 1024, an A/B) partitions in its own tiles with the separate histogram pass.
+// Per plan (upload_plan): 28672 for changesets of >= 4 such tiles on average (the fan-in: a tie with 14336,
+// profiles/r04_l1tile_fused_ab.txt), 14336 for smaller ones, whose last, partial tile is then a smaller
+// share (cfg3, ~98K records per changeset: 3.020 vs 3.051 ms, r04_cfg3_l1tile_ab.txt).
 constexpr uint32_t kL1TileDefault = 28672;
-inline uint32_t l1_plan_tile(const crdt_ctx* c) {
-    return c->l1_tile == 14336u || c->l1_tile == 28672u ? c->l1_tile : kL1TileDefault;
+inline uint32_t l1_choose(const crdt_ctx* c, uint32_t R, uint64_t n) {
+    if (c->l1_tile == 14336u || c->l1_tile == 28672u) return c->l1_tile;
+    return R && n / R < 4ull * kL1TileDefault ? 14336u : kL1TileDefault;
 }
+inline uint32_t l1_plan_tile(const crdt_ctx* c) { return c->plan_l1_tile; }
 
 
 namespace {
@@ -1899,6 +1905,7 @@ int upload_plan(crdt_ctx* c, const crdt_batch* b, uint64_t* tiles_out, uint32_t*
     uint32_t* h_ptb = reinterpret_cast<uint32_t*>(c->h_plan.p + (R + 1) + half);
     uint64_t tiles = 0, ptiles = 0;
     uint32_t mt = 0;
+    c->plan_l1_tile = l1_choose(c, R, b->offsets[R] - b->offsets[0]);
     for (uint32_t j = 0; j <= R; ++j) {
         h_offs[j] = b->offsets[j];
         h_tstart[j] = (uint32_t)tiles;
@@ -2406,7 +2413,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         uint32_t nt1 = 0;
         // level-1 tile (CRDT_L1_TILE, A/B): kPTile, whose level-1 histogram the scan counts; another size
         // (a multiple of 1024) takes the histogram pass
-        const uint32_t l1t = anchor ? l1_plan_tile(c) : c->l1_tile ? c->l1_tile : kL1TileDefault;
+        const uint32_t l1t = anchor || !c->l1_tile ? l1_plan_tile(c) : c->l1_tile;
         for (uint32_t s = 0; s <= nseg; ++s) {
             tb[s] = nt1;
             if (s < nseg) {
