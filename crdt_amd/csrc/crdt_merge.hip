@@ -28,7 +28,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <mutex>
 #include <new>
 #include <vector>
 
@@ -122,8 +121,6 @@ struct Misc {
     uint32_t err;          // key range violation
     uint32_t vdone;        // k_verify<true> workgroups finished (the last one resolves)
     uint32_t tiles_hot;    // scan tiles holding a record above C_0, every kHotSample-th (next scan's form)
-    uint32_t miss;         // anchored frame (sorted_path.inc): max of ~j over the changesets j holding a
-                           // record below the frame (0: none) — the frame is invalid if one is applied
     crdt_result result;    // filled by k_resolve
     // frame of the batch's records (k_scan<*, *, true>) for the sorted path's packed key
     // (sorted_path.inc), as max-accumulators whose identity is the memset's 0:
@@ -138,6 +135,9 @@ struct Misc {
     unsigned long long route_own;   // k_route_plan: bit 0 = the own chunk is scattered into the receive columns;
                                     // bit 1 = the send counts do not add up to the batch (the scatters exit);
                                     // bit 2 (k_shard_combine) = the ranks' collective-shape words differ
+    unsigned long long shard_status; // k_shard_combine: the largest local failure code (-CRDT_E_*) any rank put in
+                                     // its gather row (0: none) — every rank fails the call with it
+    unsigned long long pad_;
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
@@ -633,8 +633,7 @@ __global__ __launch_bounds__(64) void k_verify(
     long long* __restrict__ event, int64_t c0, const int64_t* __restrict__ Rj, const int64_t* __restrict__ Cj,
     uint32_t tile_recs)
 {
-    // tile_recs: records per tile of T / tstart / cand_tile (kTile for the scan's tiles, kPTile for the
-    // level-1 partition tiles of the anchored sorted path, whose scatter reduces the tile maxima).
+    // tile_recs: records per tile of T / tstart / cand_tile (kTile, the scan's tiles).
     // pbase / ibase (optional): this ctx holds only a PART of changeset j, preceded in
     // its iteration order by records of other ranks whose max lt is pbase[j] and whose
     // count is ibase[j] (key-sharded "parts" protocol, crdt_amd/dist.py).
@@ -1137,12 +1136,12 @@ __global__ __launch_bounds__(256) void k_flags_back(const uint8_t* __restrict__ 
 
 // Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j, and
 // gsend[2R .. 2R + 4) = this rank's record frame (Misc::fr_*, max-accumulators).
-constexpr uint32_t kGatherExtra = 5;     // the frame's 4 words, then the rank's collective-shape word
+constexpr uint32_t kGatherExtra = 6;     // the frame's 4 words, the rank's collective-shape word, its local status
 // gsend[2R + 4] = cfg: the per-process settings that shape the collectives after the clock phase
 // (comm_path.inc, shard_cfg_word); k_shard_combine checks that every rank sent the same one.
 __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict__ offs, uint32_t R,
                                                      const Misc* __restrict__ misc, long long* __restrict__ gsend,
-                                                     long long cfg)
+                                                     long long cfg, long long status)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j < R) gsend[R + j] = (long long)(offs[j + 1] - offs[j]);
@@ -1152,6 +1151,23 @@ __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict_
         gsend[2 * R + 2] = (long long)misc->fr_rlo;
         gsend[2 * R + 3] = (long long)misc->fr_rhi;
         gsend[2 * R + 4] = cfg;
+        gsend[2 * R + 5] = status;
+    }
+}
+
+// The gather row of a rank whose local work failed before the gather (its status: -CRDT_E_*, > 0): no
+// maxima, no records, no frame — the row only carries the status to the other ranks (k_shard_combine).
+__global__ __launch_bounds__(256) void k_fail_row(long long* __restrict__ gsend, uint32_t R, long long cfg,
+                                                  long long status)
+{
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < R; j += gridDim.x * 256) {
+        gsend[j] = INT64_MIN;
+        gsend[R + j] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int x = 0; x < 4; ++x) gsend[2 * R + x] = 0;
+        gsend[2 * R + 4] = cfg;
+        gsend[2 * R + 5] = status;
     }
 }
 
@@ -1176,6 +1192,12 @@ __global__ __launch_bounds__(256) void k_shard_combine(const long long* __restri
         bool same = true;                                   // every rank's collective-shape word alike
         for (uint32_t r = 1; r < G; ++r) same = same && g[r * row + 2ull * R + 4] == g[2ull * R + 4];
         if (!same) misc->route_own = 4ull;                  // (k_route_plan has not run yet)
+        unsigned long long fs = 0;                          // a rank's local failure fails every rank
+        for (uint32_t r = 0; r < G; ++r) {
+            const unsigned long long x = (unsigned long long)g[r * row + 2ull * R + 5];
+            fs = x > fs ? x : fs;
+        }
+        misc->shard_status = fs;
     }
     if (j >= R) return;
     int64_t m = INT64_MIN, pm = INT64_MIN;
@@ -1193,16 +1215,23 @@ __global__ __launch_bounds__(256) void k_shard_combine(const long long* __restri
     ibase[j] = ib;
 }
 
-// Per-record counts and the key-range error of this rank, as SUM-reducible words.
-__global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long long* __restrict__ out)
+// Per-record counts and the key-range error of this rank, as SUM-reducible words; then one word per
+// local failure code (out[kSumWords + code] = 1 for this rank's -CRDT_E_* status, code 1..7), so the
+// reduced words tell every rank which failures occurred anywhere.
+constexpr int kSumWords = 4, kSumCodes = 8;
+__global__ void k_sum_counts(const Misc* __restrict__ misc, bool counted, long long* __restrict__ out, int status)
 {
     if (threadIdx.x != 0) return;
     unsigned long long np = 0, nw = 0;
-    for (int s = 0; s < kCounterSlots; ++s) { np += misc->present[s]; nw += misc->won[s]; }
+    if (!status)
+        for (int s = 0; s < kCounterSlots; ++s) { np += misc->present[s]; nw += misc->won[s]; }
     out[0] = (long long)np;
     out[1] = (long long)nw;
-    out[2] = misc->err ? 1 : 0;
+    out[2] = !status && misc->err ? 1 : 0;
     out[3] = counted ? 0 : 1;
+    for (int k = 0; k < kSumCodes; ++k) out[kSumWords + k] = 0;
+    if (status < 0 && -status < kSumCodes) out[kSumWords - status] = 1;
+    else if (status < 0) out[kSumWords + kSumCodes - 1] = 1;
 }
 
 // Key ids against the capacity before any row is stored (resident batches of the gather path;
@@ -1413,118 +1442,15 @@ static bool poison_alloc() {
     static const int v = [] { const char* e = getenv("CRDT_POISON_ALLOC"); return e && atoi(e) ? 1 : 0; }();
     return v != 0;
 }
-// CRDT_ALLOC_CONTIG=1: the partition buffers (the level-1 / level-2 scatters' scattered destinations) are
-// allocated physically contiguous (hipDeviceMallocContiguous; plain hipMalloc if that fails) — the
-// placement experiment of DESIGN §6 (the level-1 scatter's process-to-process spread).
-static bool contig_alloc() {
-    static const int v = [] { const char* e = getenv("CRDT_ALLOC_CONTIG"); return e && atoi(e) ? 1 : 0; }();
-    return v != 0;
-}
-
-// CRDT_ALLOC_SHUFFLE=1: the partition buffers are assembled from separately created physical chunks of
-// CRDT_SHUFFLE_KB (default 2048) mapped into one virtual range in a fixed pseudo-random order (the HIP
-// virtual-memory API), so their physical placement no longer depends on the allocator's state — the second
-// placement experiment of DESIGN §6.  Freed through vmm_free (DBuf::vmm).
-struct VmmRange {
-    size_t bytes = 0;
-    std::vector<hipMemGenericAllocationHandle_t> chunks;
-};
-static std::mutex g_vmm_mu;
-static std::vector<std::pair<void*, VmmRange>> g_vmm;
-
-static bool shuffle_alloc() {
-    static const int v = [] { const char* e = getenv("CRDT_ALLOC_SHUFFLE"); return e && atoi(e) ? 1 : 0; }();
-    return v != 0;
-}
-
-static hipError_t vmm_shuffled_alloc(void** out, size_t bytes) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = dev;
-    size_t gran = 0;
-    if ((e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum)) != hipSuccess) return e;
-    size_t chunk = (size_t)2 << 20;
-    if (const char* v = getenv("CRDT_SHUFFLE_KB")) chunk = (size_t)std::max(atoi(v), 4) << 10;
-    chunk = (chunk + gran - 1) / gran * gran;
-    const size_t nch = (bytes + chunk - 1) / chunk, total = nch * chunk;
-    void* va = nullptr;
-    if ((e = hipMemAddressReserve(&va, total, chunk, nullptr, 0)) != hipSuccess) return e;
-    VmmRange r;
-    r.bytes = total;
-    std::vector<size_t> perm(nch);
-    for (size_t i = 0; i < nch; ++i) perm[i] = i;
-    uint64_t x = 0x9E3779B97F4A7C15ull ^ nch;                      // fixed order (splitmix64 Fisher-Yates)
-    for (size_t i = nch; i > 1; --i) {
-        x += 0x9E3779B97F4A7C15ull;
-        uint64_t z = x;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        z ^= z >> 31;
-        std::swap(perm[i - 1], perm[z % i]);
-    }
-    for (size_t i = 0; i < nch && e == hipSuccess; ++i) {
-        hipMemGenericAllocationHandle_t h;
-        if ((e = hipMemCreate(&h, chunk, &prop, 0)) != hipSuccess) break;
-        r.chunks.push_back(h);
-        e = hipMemMap(static_cast<char*>(va) + perm[i] * chunk, chunk, 0, h, 0);
-    }
-    if (e == hipSuccess) {
-        hipMemAccessDesc acc{};
-        acc.location = prop.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        e = hipMemSetAccess(va, total, &acc, 1);
-    }
-    if (e != hipSuccess) {
-        hipMemUnmap(va, total);
-        for (auto h : r.chunks) hipMemRelease(h);
-        hipMemAddressFree(va, total);
-        return e;
-    }
-    std::lock_guard<std::mutex> g(g_vmm_mu);
-    g_vmm.emplace_back(va, std::move(r));
-    *out = va;
-    return hipSuccess;
-}
-
-static void vmm_free(void* va) {
-    VmmRange r;
-    {
-        std::lock_guard<std::mutex> g(g_vmm_mu);
-        for (size_t i = 0; i < g_vmm.size(); ++i)
-            if (g_vmm[i].first == va) {
-                r = std::move(g_vmm[i].second);
-                g_vmm.erase(g_vmm.begin() + (ptrdiff_t)i);
-                break;
-            }
-    }
-    if (!r.bytes) return;
-    hipDeviceSynchronize();                         // (hipFree's implicit wait, which unmapping lacks)
-    hipMemUnmap(va, r.bytes);
-    for (auto h : r.chunks) hipMemRelease(h);
-    hipMemAddressFree(va, r.bytes);
-}
-
 template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
-    bool vmm = false;               // p came from vmm_shuffled_alloc
-    hipError_t ensure(size_t want, bool contig = false) {
+    hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
         if (p) release();
         size_t m = std::max<size_t>(want, 16);
-        hipError_t e = hipErrorMemoryAllocation;
-        if (contig && shuffle_alloc()) {
-            e = vmm_shuffled_alloc(reinterpret_cast<void**>(&p), m * sizeof(T));
-            vmm = e == hipSuccess;
-        }
-        if (e != hipSuccess && contig && contig_alloc())
-            e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p), m * sizeof(T), hipDeviceMallocContiguous);
-        if (e != hipSuccess) e = hipMalloc(&p, m * sizeof(T));
+        hipError_t e = hipMalloc(&p, m * sizeof(T));
         if (e == hipSuccess) n = m;
         if (e == hipSuccess && poison_alloc()) {      // (finished before any stream's next use)
             e = hipMemset(p, 0x5A, m * sizeof(T));
@@ -1533,11 +1459,9 @@ struct DBuf {
         return e;
     }
     void release() {
-        if (p && vmm) vmm_free(p);
-        else if (p) hipFree(p);
+        if (p) hipFree(p);
         p = nullptr;
         n = 0;
-        vmm = false;
     }
 };
 
@@ -1568,6 +1492,9 @@ struct Rl1Scratch {
     DBuf<u32x4> rec2;
     DBuf<uint64_t> plan;
     HBuf<uint64_t> hplan;
+    size_t pw = 0, u32w = 0;        // the plan's words (rl1_owner_prep)
+    uint32_t nt2 = 0, nc2 = 0;      // level-2 tiles and scan chunks
+    uint64_t nw = 0;                // records of the piece at this owner
     void release() {
         hist.release(); toff.release(); part.release(); choff.release(); dstart2.release(); tseg.release();
         ibase.release(); ibucket.release(); ksu32.release(); kj2.release(); kslt.release(); rec2.release();
@@ -1598,9 +1525,8 @@ constexpr uint32_t kFormNoVecLoads = 8192;   // level-1 scatter: one 4/8-B load 
 constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histogram): strided 8 / 4-B loads
 constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
-constexpr uint32_t kFormAnchor = 262144;     // the anchored sorted path ON (merge_anchored; off by default:
-                                             // measured 0.25 ms slower per fan-in step)
 constexpr uint32_t kFormNoOwnInPlace = 524288; // sharded merge: the own chunk copied to the receive columns
+constexpr uint32_t kPartPad = 1024;          // records of slack behind every partition buffer (tile-end vector loads)
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
 struct crdt_ctx {
@@ -1672,6 +1598,7 @@ struct crdt_ctx {
     int place_trial = 0;               // trials done (-1: the warm-up merge comes first); candidate = trial % k,
                                        // two rounds (the clocks still settle over the first merges)
     int place_best = -1;               // the kept candidate (-1: trials not done)
+    int place_idle = 0;                // merges since the trials were asked for that did not take the sorted path
     float place_ms[kPlaceMax] = {};    // each candidate's level-1 scatter (ms; the faster of its two trials)
     bool place_timed = false;          // this call times candidate place_trial
     bool place_warm = false;           // this call is the untimed warm-up (the kernels' first launch loads them)
@@ -1692,7 +1619,6 @@ struct crdt_ctx {
     bool frame_on = false;          // this plan's scan reduced the record frame into misc->fr_*
     uint32_t rank_bound = 0;        // crdt_set_rank_bound: every rank < bound (0: unknown)
     uint32_t form_off = 0;
-    uint32_t l1_shift_kb = 0, l2_shift_kb = 0;   // CRDT_L1_SHIFT / CRDT_L2_SHIFT (KB, < 4096)          // CRDT_SORTED_FORM: packed-form refinements switched off (A/B runs)
     bool env_dynamic = false;
     bool hist_fuse = true;          // CRDT_HIST_FUSE=0: the level-1 histogram as its own pass
     uint32_t l1_tile = 0;           // CRDT_L1_TILE: the level-1 tile in records (0 = chosen per plan: l1_choose)
@@ -1704,26 +1630,19 @@ struct crdt_ctx {
     uint64_t plan_ptiles = 0;
     DBuf<uint32_t> p_hist1;
     bool hist1_fused = false;
+    bool hist1_routed = false;      // ... counted with route_l1's key map (owner-major digits), for route_l1 only
     const uint32_t* hist1_key = nullptr;
     uint32_t hist1_shift = 0;
     bool last_packed = false;       // the last sorted apply used the packed form
-    bool anchored = false;          // this call runs the anchored sorted path (merge_anchored)
     bool last_wire_pk = false;      // the last sharded merge routed 16-B packed records
     bool last_own_in_place = false; // ... and scattered its own chunk into the receive columns
-    bool last_anchored = false;
-    uint32_t anchor_skip = 0;       // calls left before the anchored frame is tried again after a miss
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
     bool last_hw = false;           // ... whose packed resolve skipped the rows >= hw_read
     // per-record win flags on the sorted path (the flagged form, sorted_path.inc): CRDT_FLAGS_SORTED=0
     // keeps every flagged merge on the gather path
     bool flags_sorted = true;
-    int pf_threads = 1024;          // CRDT_PF_THREADS: the ordered resolve's workgroup (1024 or 512)
-    int flag_bits = 0;              // CRDT_FLAG_BITS: 1 the flagged form's level-1 flags as bits, 2 level 2's too
-                                    // (measured slower, DESIGN §5.4: opt-in)
-    bool pf_head32 = false;         // CRDT_PF_HEAD32=1: its list heads 32-bit (one workgroup per CU)
     int fback_chk = 6;              // CRDT_FBACK_CHK = 0 / 4 / 6: the flag passes' run-search checkpoints (A/B)
-    int l2_items = 8;               // CRDT_L2_ITEMS=4: the packed level-2 scatter's 4-record sub-tiles (A/B)
     bool last_flagged = false;      // the last sorted apply was the flagged form
     int combine = 1;                // sharded order-free fan-ins fold home records before routing (CRDT_COMBINE:
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
@@ -1794,7 +1713,15 @@ struct crdt_ctx {
     DBuf<uint64_t> r_perm;
     DBuf<uint8_t> r_flags, r_sflags;
     HBuf<uint8_t> h_stage;                                // CRDT_MEM_HOST backends
-    HBuf<long long> h_sum;                                // reduced counts / error / uncounted
+    HBuf<long long> h_sum;                                // reduced counts / error / uncounted / failure codes
+    // failures agreed over the ranks (comm_path.inc): comm_agree's word, route_l1's count exchange
+    DBuf<long long> d_agree;
+    HBuf<long long> h_agree;
+    DBuf<unsigned long long> d_rl1cnt;                    // route_l1: [2][G][P][D] counts, then the status word
+    HBuf<uint64_t> h_rl1cnt;
+    bool finish_posted = false;                           // this call's finish_apply posted its reduction
+    // CRDT_TEST_FAIL="rank:point" (tests): this rank fails with CRDT_E_NOMEM at that point of a sharded merge
+    int fail_rank = -1, fail_at = 0;
 };
 
 // The level-1 partition tile (records).  The default and 14336 / 28672 are tiles the scan's fused histogram
@@ -1942,9 +1869,6 @@ inline size_t events_for(size_t nsegs) {     // (windows 1..3 also bracket the s
     return std::max(ev_window(nsegs / kTimingStride + 2, true), ev_window(3, true)) + 1;
 }
 
-// finish_apply: the anchored frame missed (a record below it in an applied changeset); internal
-constexpr int kAnchorRetry = 1000;
-
 inline void raise_hw(crdt_ctx* c, uint64_t key_end) {
     c->hw = std::max<uint64_t>(c->hw, std::min<uint64_t>(key_end, c->cap));
 }
@@ -2001,6 +1925,7 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
     if (hist || rhist) {
         HIPALLOC(c->p_hist1.ensure(c->plan_ptiles * kDigits));
         c->hist1_fused = true;
+        c->hist1_routed = rhist;
         c->hist1_key = home->key_id;
         c->hist1_shift = rhist || c->cap > (1ull << 20) ? 20u : (uint32_t)kSBits;
     }
@@ -2156,23 +2081,28 @@ PackFrame frame_of(const crdt_ctx* c) {
 // Read the call's outcome back (one D2H of Misc, the only sync of the apply phase).  On a
 // sharded ctx the per-record counts, the key-range error and "not counted" are SUM-reduced
 // over the ranks first, so every rank returns the same result.
+// local_st (a sharded ctx): this rank's apply failed before its end (-CRDT_E_*); the SUM reduction is posted
+// all the same, carrying the failure, so every rank returns the same status (comm_path.inc).
 int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64_t n, bool sorted,
-                 crdt_result* out) {
+                 crdt_result* out, int local_st = 0) {
     // the order-free sorted form does not count them (the flagged form does)
     const bool counted = !sorted || c->counts || c->last_flagged;
-    if (c->has_comm) {
-        HIPALLOC(c->d_sum.ensure(4));
-        HIPALLOC(c->h_sum.ensure(4));
-        k_sum_counts<<<1, 64, 0, c->stream>>>(c->d_misc, counted, c->d_sum.p);
-        int st = comm_all_reduce(c, c->d_sum.p, 4, CRDT_REDUCE_SUM);
+    if (c->has_comm) {                      // (d_sum / h_sum: allocated by comm_attach)
+        c->finish_posted = true;
+        k_sum_counts<<<1, 64, 0, c->stream>>>(c->d_misc, counted, c->d_sum.p, local_st);
+        int st = comm_all_reduce(c, c->d_sum.p, kSumWords + kSumCodes, CRDT_REDUCE_SUM);
         if (st) return st;
-        HIPCHK(hipMemcpyAsync(c->h_sum.p, c->d_sum.p, 4 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_sum.p, c->d_sum.p, (kSumWords + kSumCodes) * sizeof(long long),
+                              hipMemcpyDeviceToHost, c->stream));
+    } else if (local_st) {
+        return local_st;
     }
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-    if (host_flags && n) HIPCHK(hipMemcpyAsync(host_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
+    if (host_flags && n && !local_st) HIPCHK(hipMemcpyAsync(host_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->anchored && c->h_misc->miss != 0 && 0xFFFFFFFFu - c->h_misc->miss < c->h_misc->stop)
-        return kAnchorRetry;                    // nothing stored, canonical untouched: rerun exactly
+    if (c->has_comm)                        // a rank's failure (the largest code) is every rank's
+        for (int k = kSumCodes - 1; k > 0; --k)
+            if (c->h_sum.p[kSumWords + k]) return -k;
     crdt_result res = c->h_misc->result;
     c->scan_eager = 2ull * kHotSample * c->h_misc->tiles_hot > c->plan_tiles;
     if (c->key_end_valid && !c->has_comm)        // rows stored lie in the sorted path's buckets
@@ -2325,15 +2255,46 @@ void prof_resolve_report() {
 }
 #endif
 
+// PlaceTune's candidate level-1 buffers (crdt_reserve_scratch asked for c->place_k of them), taken by the
+// warm-up merge with that call's form and size: extra candidates only while they stay within 1/8 of the
+// device's HBM together and leave a quarter of it free (at the 1B fan-in: two of 14 GB); the candidates
+// that fit are timed, the rest dropped.
+void place_take(crdt_ctx* c, size_t rec_units, size_t kj_units) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = total_b = 0;
+    const size_t cb = rec_units * sizeof(u32x4) + kj_units * sizeof(uint32_t);
+    size_t used = 0;
+    int k = 1;
+    for (; k < c->place_k; ++k) {
+        if (used + cb > total_b / 8 || free_b < used + cb + total_b / 4) break;
+        if (c->pc_rec[k].ensure(rec_units) != hipSuccess || c->pc_kj[k].ensure(kj_units) != hipSuccess) {
+            c->pc_rec[k].release();
+            c->pc_kj[k].release();
+            break;
+        }
+        used += cb;
+    }
+    c->place_k = k;
+    if (k == 1) {                                      // nothing to try: p1 stays
+        c->place_trial = 0;
+        c->place_best = 0;
+    }
+}
+
+// A ctx that asked for placement trials but whose merges do not take the sorted path: the candidates go.
+void place_drop(crdt_ctx* c) {
+    for (int i = 1; i < crdt_ctx::kPlaceMax; ++i) { c->pc_rec[i].release(); c->pc_kj[i].release(); }
+    c->place_k = 1;
+    c->place_trial = 0;
+    c->place_best = 0;
+}
+
 // Sorted path (sorted_path.inc) for the whole batch: k_resolve (stop point), then per
 // window of kWindow changesets a level-1 (+ level-2) partition of the applied records and
 // the per-bucket LDS resolve.  sg = the batch's changeset segments (host), in changeset
 // order; one changeset may be several segments (records routed in from several ranks).
-// anchor (merge_anchored): the packed form on the frame given, one window, and the clock phase
-// (tile maxima from the level-1 scatter, recurrence, exception scan, stop point) run between the
-// level-1 scatter and level 2 instead of before this function.
 int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, const long long* d_event,
-                 crdt_result* out, const PackFrame* anchor = nullptr, uint8_t* dflags = nullptr,
+                 crdt_result* out, uint8_t* dflags = nullptr,
                  EmitOut* emit = nullptr) {
     const uint32_t R = c->plan_R;
     // dflags (device, zeroed by the caller): the flagged form — packed records, stable level 2, the
@@ -2343,10 +2304,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     // the key range and hw_read = 0) and emit one packed maximum per key; no row, result or timing
     const bool em = emit != nullptr;
     if (!em) {
-        if (!c->resolved && !anchor)
+        if (!c->resolved)
             k_resolve<<<1, 64, 0, c->stream>>>(d_event, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
         c->resolved = false;
-        if (!anchor) ev_record(c, kEvApply);
+        ev_record(c, kEvApply);
         c->windows.clear();
         c->apply_total = 1;
         if (c->timing) ev_record(c, ev_window(0, false));
@@ -2358,20 +2319,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     // batch fits the 64-bit key (one read-back of Misc per call), else wide payloads + lists
     PackFrame pf{};
     bool pk = false;
-    if (anchor) {
-        pf = *anchor;
-        pk = true;
-    } else if (cols.packed_in || (c->packed_resolve && c->frame_on)) {
+    if (cols.packed_in || (c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         pf = frame_of(c);
         pk = pf.ok;
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
     }
-    if ((fl || em) && (!pk || anchor || cols.packed_in)) return CRDT_E_INVALID;   // the callers checked the frame
+    if ((fl || em) && (!pk || cols.packed_in)) return CRDT_E_INVALID;   // the callers checked the frame
     // the ordered packed form: the flagged form's kernels, for win flags and / or exact per-record
     // counts (without flags: no positions kept, no flags carried back)
-    const bool ord = !em && (fl || (c->counts && pk && !anchor && !cols.packed_in));
+    const bool ord = !em && (fl || (c->counts && pk && !cols.packed_in));
     c->last_ordered = ord;
     c->last_packed = pk;
     c->key_end_valid = true;                 // k_bucket_items bounds the rows every window writes
@@ -2413,7 +2371,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         uint32_t nt1 = 0;
         // level-1 tile (CRDT_L1_TILE, A/B): kPTile, whose level-1 histogram the scan counts; another size
         // (a multiple of 1024) takes the histogram pass
-        const uint32_t l1t = anchor || !c->l1_tile ? l1_plan_tile(c) : c->l1_tile;
+        const uint32_t l1t = !c->l1_tile ? l1_plan_tile(c) : c->l1_tile;
         for (uint32_t s = 0; s <= nseg; ++s) {
             tb[s] = nt1;
             if (s < nseg) {
@@ -2440,16 +2398,24 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         HIPALLOC(c->p_part.ensure((size_t)ncm * kDigits));
         HIPALLOC(c->p_choff.ensure((size_t)ncm * kDigits));
         HIPALLOC(c->p_dstart1.ensure(kDigits + 1));
-        // partition buffers, each base shifted by the CRDT_L{1,2}_SHIFT knob (KB; placement A/B runs)
-        constexpr size_t kShiftPad = 4u << 20;                      // bytes
+        // the partition buffers hold this form's records: packed payloads 12 B (Rec12), key columns 2 B at
+        // level 1 (k16) and 1 B at level 2 (k8); the wide form 16 + 4 B
+        const size_t rec_units = (pk ? (3 * (size_t)nw + 3) / 4 : (size_t)nw) + kPartPad;      // u32x4
+        const size_t kj1_units = (k16 ? ((size_t)nw + 1) / 2 : (size_t)nw) + kPartPad;          // uint32
+        const size_t kj2_units = (k8 ? ((size_t)nw + 3) / 4 : (size_t)nw) + kPartPad;
         // a placement trial (PlaceTune): candidate place_trial stands in as p1 for this call, every window
-        // of it (swapped back in place_finish)
-        if (c->place_k > 1 && c->place_trial < 0 && !c->has_comm && s0 == 0) c->place_warm = true;
-        if (c->place_k > 1 && c->place_trial >= 0 && c->place_trial < 2 * c->place_k && !c->has_comm && s0 == 0) {
+        // of it (swapped back in place_finish); the candidates are taken by the warm-up merge, sized for its
+        // form and capped (place_take)
+        if (c->place_k > 1 && c->place_trial < 0 && !c->has_comm && s0 == 0 && !c->place_warm) {
+            c->place_warm = true;
+            place_take(c, rec_units, kj1_units);
+        }
+        if (c->place_k > 1 && c->place_trial >= 0 && c->place_trial < 2 * c->place_k && !c->has_comm && s0 == 0 &&
+            !c->place_timed) {
             const int k = c->place_trial % c->place_k;
             if (k) {                                  // (grown like p1 itself when this call holds more records)
-                HIPALLOC(c->pc_rec[k].ensure(nw + kShiftPad / 16, true));
-                HIPALLOC(c->pc_kj[k].ensure(nw + kShiftPad / 4, true));
+                HIPALLOC(c->pc_rec[k].ensure(rec_units));
+                HIPALLOC(c->pc_kj[k].ensure(kj1_units));
                 std::swap(c->p1_rec, c->pc_rec[k]);
                 std::swap(c->p1_kj, c->pc_kj[k]);
             }
@@ -2457,9 +2423,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 if (!e) HIPCHK(hipEventCreate(&e));
             c->place_timed = true;
         }
-        HIPALLOC(c->p1_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p1_kj.ensure(nw + kShiftPad / 4, true));
-        u32x4* p1r = c->p1_rec.p + (size_t)c->l1_shift_kb * 64;
-        uint32_t* p1k = c->p1_kj.p + (size_t)c->l1_shift_kb * 256;
+        HIPALLOC(c->p1_rec.ensure(rec_units)); HIPALLOC(c->p1_kj.ensure(kj1_units));
+        u32x4* p1r = c->p1_rec.p;
+        uint32_t* p1k = c->p1_kj.p;
         u32x4* p2r = nullptr;
         uint32_t* p2k = nullptr;
         const uint64_t* d_beg = c->p_plan.p;
@@ -2474,13 +2440,15 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (two) HIPALLOC(c->p_l1beg.ensure(kDigits + 1));
         // level-1 histogram: counted by the scan (then only the changesets >= stop are cleared)
         // or here
-        const bool h1 = !anchor && c->hist1_fused && s0 == 0 && se == ns_all && !cols.packed_in &&
-                        cols.key == c->hist1_key && c->hist1_shift == shift1 && nt1 == c->plan_ptiles;
+        // (the same key map — not route_l1's owner-major one, ADVICE r4 — and the same tile boundaries)
+        const bool h1 = c->hist1_fused && !c->hist1_routed && s0 == 0 && se == ns_all && !cols.packed_in &&
+                        cols.key == c->hist1_key && c->hist1_shift == shift1 && nt1 == c->plan_ptiles &&
+                        l1t == l1_plan_tile(c);
         const uint32_t* hist1 = h1 ? c->p_hist1.p : c->p_hist.p;
         if (h1)
             k_hist_trim<<<256, 256, 0, c->stream>>>(c->p_hist1.p, c->d_ptb, R, c->d_misc);
-        else                                        // (anchored: every changeset, stop not known yet)
-            k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, anchor ? nullptr : c->d_misc,
+        else
+            k_part_hist<true><<<nt1, kHThreads, 0, c->stream>>>(cols.key, tm1, jb, c->d_misc,
                                                                  c->cap, shift1, c->p_hist.p);
         c->last_hist1_fused = h1;
         k_scan_part<<<nc1, 256, 0, c->stream>>>(hist1, sm1, c->p_part.p);
@@ -2488,75 +2456,46 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                              two ? c->p_l1beg.p : nullptr);
         k_scan_tiles<<<nc1, 256, 0, c->stream>>>(hist1, c->p_choff.p, sm1, c->p_dstart1.p, c->p_toff.p);
         const bool ph = c->timing && s0 == 0 && !em;   // phase events: the first window
-        if (anchor) ev_record(c, kEvScan);          // (anchored: the keys-only histogram pass and its scans)
         if (ph) ev_record(c, ev_window(1, false));
         if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));   // (the first window)
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
-        const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
-        const AnchorArgs an{c->d_T.p, c->d_candtile.p, wsub(imax(c->canonical, wp), pf.lt0), c->local_rank};
         if (fl && k16)          // the flagged form: each record's level-1 position kept at its input index
-            k_part_scatter1<true, false, true, kL1Items, true, true, false, true>
+            k_part_scatter1<true, false, true, kL1Items, true, true, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p, hist1);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, c->f_pos1.p, hist1);
         else if (fl)
-            k_part_scatter1<true, false, false, kL1Items, true, false, false, true>
+            k_part_scatter1<true, false, false, kL1Items, true, false, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{}, c->f_pos1.p, hist1);
-        else if (anchor && k16)
-            k_part_scatter1<true, false, true, kL1AnchorItems, true, true, true>
-                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, an);
-        else if (anchor)
-            k_part_scatter1<true, false, false, kL1AnchorItems, true, false, true>
-                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
-                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, an);
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, c->f_pos1.p, hist1);
         else if (cols.packed_in && k16)
             k_part_scatter1<true, true, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (cols.packed_in)
             k_part_scatter1<true, true, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (k16 && !(c->form_off & kFormNoVecLoads))
             k_part_scatter1<true, false, true, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (k16)
             k_part_scatter1<true, false, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else if (pk)
             k_part_scatter1<true, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         else
             k_part_scatter1<false, false, false, kL1Items, true><<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
-                p1k, xper1, pf, rev1 ? hist1 : nullptr, AnchorArgs{});
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
         if (ph) ev_record(c, ev_window(1, true));
         if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[1], c->stream));
-        if (anchor) {
-            // the clock phase on the scatter's tile maxima (level-1 tiles of kPTile records): M_j,
-            // the recurrence, the exact exception scan of candidate tiles, stop point and canonical
-            k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_ptb, R, c->d_M.p);
-            k_clock<false><<<1, 1024, 0, c->stream>>>(c->d_M.p, nullptr, nullptr, R, wall, c->canonical,
-                                                      c->d_Cprev.p, c->d_Rj.p, c->d_Cj.p, c->d_event.p);
-            k_verify<false><<<kVerifyBlocks, 64, 0, c->stream>>>(
-                cols.lt, cols.rank, nullptr, c->d_offs, c->d_ptb, R, c->d_T.p, c->d_Cprev.p, wall, c->local_rank,
-                c->d_misc, c->d_candtile.p, c->d_candkey.p, c->d_candP.p, c->d_candkind.p, c->d_candms.p, nullptr,
-                nullptr, c->d_event.p, 0, nullptr, nullptr, l1t);
-            k_resolve_local<<<1, 256, 0, c->stream>>>(c->d_misc, c->d_candkey.p, c->d_candP.p, c->d_candkind.p,
-                                                      c->d_candms.p, c->d_event.p);
-            k_resolve<<<1, 64, 0, c->stream>>>(c->d_event.p, R, wall, c->canonical, c->d_Rj.p, c->d_Cj.p, c->d_misc);
-            ev_record(c, kEvClock);
-            ev_record(c, kEvApply);
-        }
         if (ph) ev_record(c, ev_window(2, false));
         TileMap tm2f{};                              // level 2's tiling and counts (the flag pass)
         uint32_t nt2f = 0;
@@ -2565,9 +2504,9 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (two) {
             HIPALLOC(c->p_l2map.ensure(2 * (kDigits + 1)));
             HIPALLOC(c->p_dstart2.ensure(kDigits * kDigits + 1));
-            HIPALLOC(c->p2_rec.ensure(nw + kShiftPad / 16, true)); HIPALLOC(c->p2_kj.ensure(nw + kShiftPad / 4, true));
-            p2r = c->p2_rec.p + (size_t)c->l2_shift_kb * 64;
-            p2k = c->p2_kj.p + (size_t)c->l2_shift_kb * 256;
+            HIPALLOC(c->p2_rec.ensure(rec_units)); HIPALLOC(c->p2_kj.ensure(kj2_units));
+            p2r = c->p2_rec.p;
+            p2k = c->p2_kj.p;
             uint32_t* tb2 = c->p_l2map.p;
             uint32_t* cb2 = c->p_l2map.p + kDigits + 1;
             // level-2 tiles of the packed form: kPTile2 records (one sub-tile each) — 256 workgroups
@@ -2628,13 +2567,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                     p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
             else if (pk)
                 if (k16)
-                    if (c->l2_items == 4)
-                        k_part_scatter2<false, true, true, true, true, 4><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0,
-                                                                           c->stream>>>(
-                            p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
-                    else
-                        k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
-                            p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
+                    k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
                 else if (k8)
                     k_part_scatter2<false, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
@@ -2715,14 +2649,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             HIPALLOC(c->f_cin_key.ensure(ksn));
             HIPALLOC(c->f_cin_val.ensure(ksn));
             HIPALLOC(c->f_cin_pres.ensure(ksn));
-            // opt-in (CRDT_FLAG_BITS=1): the flags in level-1 order as bits between the two flag passes, two
-            // levels; 2: the level-2 flags of the resolve too.  Measured slower: the bit output of
-            // the first pass loads one 2-B position per lane, and the resolve's bit buffers spill registers
-            const bool fbits = fl && two && c->flag_bits != 0;
-            const bool fbits2 = fbits && c->flag_bits == 2 && !c->pf_head32;
             if (fl) HIPALLOC(c->f_flag2.ensure(nw + 8));
             uint8_t* fl2 = fl ? c->f_flag2.p : nullptr;
-            if (fbits2) HIPCHK(hipMemsetAsync(fl2, 0, ((nw + 31) / 32) * 4, c->stream));
             if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
@@ -2735,34 +2663,21 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
                 reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
-#define CRDT_PFLAGS(K8, T)                                                                                  \
-    if (c->pf_head32) k_resolve_pflags<K8, T, true><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb,           \
-        c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink, c->f_cin_val.p,        \
-        c->f_cin_pres.p, pf, c->d_misc, fl2);                                                                   \
-    else if (c->flag_bits == 2) k_resolve_pflags<K8, T, false, true><<<max_items, T, 0, c->stream>>>(bst,    \
-        d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,             \
-        c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);                                                   \
-    else k_resolve_pflags<K8, T><<<max_items, T, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, \
-                                                            c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,  \
-                                                            c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2)
-            if (c->pf_threads == 512) {
-                if (k8) { CRDT_PFLAGS(true, 512); } else { CRDT_PFLAGS(false, 512); }
-            } else {
-                if (k8) { CRDT_PFLAGS(true, 1024); } else { CRDT_PFLAGS(false, 1024); }
-            }
-#undef CRDT_PFLAGS
+            if (k8)
+                k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
+                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);
+            else
+                k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
+                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);
             // flags back: level-2 order -> level-1 order (two levels) -> input order
             const uint8_t* f1 = c->f_flag2.p;
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw + 8));
 #define CRDT_FBACK2(CHK)                                                                                  \
-    if (fbits2) k_flags_back<false, CHK, true, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, \
-                                                          c->f_flag2.p, c->f_flag1.p, c->d_misc);              \
-    else if (fbits) k_flags_back<false, CHK, false, true><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f,        \
-                                                          c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc); \
-    else k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,      \
+    k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,           \
                                                           c->f_flag1.p, c->d_misc)
-                if (fbits) HIPCHK(hipMemsetAsync(c->f_flag1.p, 0, ((nw + 31) / 32) * 4, c->stream));
                 if (c->fback_chk == 4) { CRDT_FBACK2(4); }
                 else if (c->fback_chk == 6) { CRDT_FBACK2(6); }
                 else { CRDT_FBACK2(0); }
@@ -2773,10 +2688,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                                                  c->p_tseg.p);
             }
 #define CRDT_FBACK1(CHK)                                                                                  \
-    if (fbits) k_flags_back<true, CHK, true><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, \
-                                                                          dflags, c->d_misc);                     \
-    else k_flags_back<true, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags,  \
-                                                             c->d_misc)
+    k_flags_back<true, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags,       \
+                                                        c->d_misc)
             if (fl) {
                 if (c->fback_chk == 4) { CRDT_FBACK1(4); }
                 else if (c->fback_chk == 6) { CRDT_FBACK1(6); }
@@ -2903,7 +2816,7 @@ int apply_segs(crdt_ctx* c, const Cols& cols, uint64_t n, int32_t mem, int64_t w
             if (n) HIPCHK(hipMemsetAsync(win_flags, 0, n, c->stream));
             c->last_flagged = true;
         }
-        return apply_sorted(c, cols, c->segs, wall, d_event, out, nullptr, win_flags);
+        return apply_sorted(c, cols, c->segs, wall, d_event, out, win_flags);
     }
     return apply_ranges(c, cols, c->segs, n, mem, wall, d_event, win_flags, out);
 }
@@ -2918,75 +2831,6 @@ int phase_apply(crdt_ctx* c, const crdt_batch* owned, int64_t wall, const long l
     if ((st = stage_apply_cols(c, owned, &cols))) return st;
     c->segs.from_offsets(owned->offsets, R);
     return apply_segs(c, cols, owned->offsets[R], owned->mem, wall, d_event, win_flags, out, allow_sorted);
-}
-
-// ---- the anchored sorted path ----------------------------------------------------------------
-// Every record a call applies has lt <= max(C_0, ((wall + 60000) << 16) | 0xFFFF) + R: recv() accepts a
-// record above the running canonical only if its millis is within 60 s of the wall clock
-// (hlc.dart:85-94; no explicit millis column, so millis = lt >> 16), and each send() adds at most one
-// (hlc.dart:58-73; by induction over the changesets).  So the packed key's lt frame can
-// be fixed before any record is read: the 2^L - 1 values up to that anchor, L = 60 - K - 13 (13-B
-// final records, K = the bits of the declared rank bound).  The clock scan's work (tile maxima,
-// candidate tiles) then rides on the level-1 scatter's own loads — no pass reads lt alone, and the
-// host does not wait for a frame — leaving a keys-only level-1 histogram as the one pre-pass.  A
-// record below the frame in an applied changeset (a replica further behind than the frame reaches)
-// makes the call store nothing (Misc::miss); the host reruns it on the scan's exact frame and leaves
-// the anchor off for the next calls of this ctx.
-bool anchored_frame(const crdt_ctx* c, uint32_t R, int64_t wall, PackFrame* out) {
-    if (!c->rank_bound) return false;
-    const int K = bitlen64(c->rank_bound);               // rank fields 0 .. bound - 1, bound = clamp
-    uint32_t jb = 0, jwin = 0;
-    if (!frame_window(60 - K - 13, K, R, &jb, &jwin) || jwin < R) return false;   // one window
-    const int L = 60 - (K + (int)jb);
-    if (L < 30) return false;                            // under ~16 s of millis: not worth a miss
-    const int64_t wp = (int64_t)(((uint64_t)(wall + kMaxDrift) << kShift) | (uint64_t)kMaxCounter);
-    const int64_t b = imax(c->canonical, wp);
-    if (b > INT64_MAX - (int64_t)R - 1) return false;
-    const int64_t top = b + (int64_t)R;
-    PackFrame f;
-    f.lt_span = (1ull << L) - 1;                         // the lt field: L bits (make_frame's rule)
-    f.lt0 = (int64_t)((uint64_t)top - f.lt_span);
-    f.rk0 = 0;
-    f.rk_span = c->rank_bound - 1;
-    f.jb = jb;
-    f.jwin = jwin;
-    f.sh = (uint32_t)K + jb;
-    f.rk_mask = (1ull << K) - 1;
-    f.rk_limit = c->rank_bound;
-    f.ok = true;
-    f.key4 = true;
-    *out = f;
-    return true;
-}
-
-// One anchored crdt_merge of resident columns (no millis column, one window of changesets); returns
-// kAnchorRetry when the frame missed (nothing stored, canonical untouched).
-int merge_anchored(crdt_ctx* c, const crdt_batch* b, int64_t wall, const PackFrame& pf, crdt_result* out) {
-    c->fused = false;
-    c->resolved = false;
-    c->hist1_fused = false;
-    const uint32_t R = b->n_changesets;
-    uint64_t tiles = 0;
-    uint32_t mt = 0;
-    int st;
-    if ((st = upload_plan(c, b, &tiles, &mt))) return st;
-    const uint64_t pt = c->plan_ptiles + 1;              // level-1 tiles: T, candidate lists
-    HIPALLOC(c->d_T.ensure(pt)); HIPALLOC(c->d_candtile.ensure(pt)); HIPALLOC(c->d_candkey.ensure(pt));
-    HIPALLOC(c->d_candP.ensure(pt)); HIPALLOC(c->d_candkind.ensure(pt)); HIPALLOC(c->d_candms.ensure(pt));
-    HIPALLOC(c->d_Cprev.ensure(R + 1)); HIPALLOC(c->d_Rj.ensure(R + 1)); HIPALLOC(c->d_Cj.ensure(R + 1));
-    if ((st = reset_misc(c))) return st;
-    c->plan_R = R;
-    c->plan_tiles = tiles;
-    c->plan_mt = mt;
-    c->frame_on = true;
-    c->frame_lt_only = true;
-    Cols cols;
-    cols.key = b->key_id; cols.lt = b->lt; cols.rank = b->rank; cols.val = b->val;
-    c->anchored = true;
-    c->last_sorted = true;
-    st = apply_sorted(c, cols, c->segs, wall, c->d_event.p, out, &pf);
-    c->anchored = false;
-    return st;
 }
 
 // After a merge's final synchronisation: the timed candidate's level-1 scatter; after the last trial, the
@@ -3036,9 +2880,6 @@ void collect_timing(crdt_ctx* c) {
             t.resolve_ms = el(ev_window(3, false), ev_window(3, true));
             t.part1_records = c->p1_records;
         }
-        // anchored: scan_ms = the keys-only level-1 histogram pass; the clock phase follows the level-1
-        // scatter, whose own time is part1_ms
-        if (c->last_anchored) t.clock_ms = std::max(0.0, t.clock_ms - t.part1_ms);
     }
     c->last_timing = t;
 }
@@ -3091,17 +2932,17 @@ static void read_env_knobs(crdt_ctx* c) {
     }
     if (const char* e = getenv("CRDT_ROUTE_TUNE")) c->route_tune = atoi(e) != 0;
     if (const char* e = getenv("CRDT_SPARSE_T")) c->sparse_t = (uint32_t)std::max(atoi(e), 0);
-    if (const char* e = getenv("CRDT_PF_THREADS")) c->pf_threads = atoi(e) == 512 ? 512 : 1024;
-    if (const char* e = getenv("CRDT_PF_HEAD32")) c->pf_head32 = atoi(e) != 0;
-    if (const char* e = getenv("CRDT_FLAG_BITS")) c->flag_bits = std::min(std::max(atoi(e), 0), 2);
-    if (const char* e = getenv("CRDT_L2_ITEMS")) c->l2_items = atoi(e) == 4 ? 4 : 8;
     if (const char* e = getenv("CRDT_FBACK_CHK")) c->fback_chk = atoi(e) == 4 ? 4 : atoi(e) == 0 ? 0 : 6;
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_L1_TILE"))
         c->l1_tile = std::min<uint32_t>((uint32_t)std::max(atoi(e), 0) / 1024u * 1024u, (uint32_t)kPTile);
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
-    if (const char* e = getenv("CRDT_L1_SHIFT")) c->l1_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
-    if (const char* e = getenv("CRDT_L2_SHIFT")) c->l2_shift_kb = std::min<uint32_t>((uint32_t)atoi(e), 4095u);
+    c->fail_rank = -1;
+    c->fail_at = 0;
+    if (const char* e = getenv("CRDT_TEST_FAIL")) {     // "rank:point" (comm_path.inc, kFail*)
+        int r = -1, at = 0;
+        if (sscanf(e, "%d:%d", &r, &at) == 2) { c->fail_rank = r; c->fail_at = at; }
+    }
 }
 
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
@@ -3133,7 +2974,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_misc, sizeof(Misc)) != hipSuccess ||
         hipHostMalloc(&c->h_misc, sizeof(Misc), hipHostMallocDefault) != hipSuccess ||
-        c->d_M.ensure(1024) != hipSuccess || c->d_event.ensure(4) != hipSuccess ||
+        c->d_M.ensure(1024) != hipSuccess || c->d_event.ensure(8) != hipSuccess ||
         c->d_word.ensure(4) != hipSuccess) {
         crdt_destroy(c);
         return CRDT_E_HIP;
@@ -3153,7 +2994,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->r_slt.release(); c->r_lt.release(); c->r_perm.release(); c->r_flags.release(); c->r_sflags.release();
     c->d_gsend.release(); c->d_grecv.release(); c->d_pbase.release(); c->d_sum.release(); c->d_tune.release(); c->h_tune.release();
     c->d_rcnt.release(); c->d_rrecv.release(); c->h_rcnt.release(); c->h_stage.release(); c->h_sum.release();
-    c->d_rcur.release();
+    c->d_rcur.release(); c->d_agree.release(); c->h_agree.release(); c->d_rl1cnt.release(); c->h_rl1cnt.release();
     if (c->route_ev) hipEventDestroy(c->route_ev);
     for (hipEvent_t e : c->rl_evs) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->rl_evx) if (e) hipEventDestroy(e);
@@ -3234,25 +3075,19 @@ int crdt_reserve_scratch(crdt_ctx* c, uint64_t n_records) {
     if (!c) return CRDT_E_INVALID;
     if (n_records == 0) return CRDT_OK;
     HIPCHK(hipSetDevice(c->device));
-    constexpr size_t kShiftPad = 4u << 20;        // as apply_sorted sizes them
-    HIPALLOC(c->p1_rec.ensure(n_records + kShiftPad / 16, true));
-    HIPALLOC(c->p1_kj.ensure(n_records + kShiftPad / 4, true));
-    HIPALLOC(c->p2_rec.ensure(n_records + kShiftPad / 16, true));
-    HIPALLOC(c->p2_kj.ensure(n_records + kShiftPad / 4, true));
-    // PlaceTune: CRDT_PLACE_TRIES candidate level-1 buffers (default 3; 1 = off), timed in the next merges
+    // sized for the packed two-level form (12-B payloads, 2-B / 1-B key columns: the fan-in's); another
+    // form grows them in its first merge
+    HIPALLOC(c->p1_rec.ensure((3 * n_records + 3) / 4 + kPartPad));
+    HIPALLOC(c->p1_kj.ensure((n_records + 1) / 2 + kPartPad));
+    HIPALLOC(c->p2_rec.ensure((3 * n_records + 3) / 4 + kPartPad));
+    HIPALLOC(c->p2_kj.ensure((n_records + 3) / 4 + kPartPad));
+    // PlaceTune: CRDT_PLACE_TRIES candidate level-1 buffers (default 3; 1 = off), taken by the next sorted
+    // merge (place_take: capped at 1/8 of HBM) and timed in the merges after it
     int tries = 3;
     if (const char* e = getenv("CRDT_PLACE_TRIES")) tries = std::min(std::max(atoi(e), 1), crdt_ctx::kPlaceMax);
     if (c->has_comm) tries = 1;                   // (a sharded ctx partitions elsewhere: route_l1, the fold)
-    for (int k = 1; k < tries; ++k) {
-        if (c->pc_rec[k].ensure(n_records + kShiftPad / 16, true) != hipSuccess ||
-            c->pc_kj[k].ensure(n_records + kShiftPad / 4, true) != hipSuccess) {
-            c->pc_rec[k].release();               // no room for more candidates: time those there are
-            c->pc_kj[k].release();
-            tries = k;
-            break;
-        }
-    }
     c->place_k = tries;
+    c->place_idle = 0;
     c->place_trial = tries > 1 ? -1 : 0;
     c->place_best = tries > 1 ? -1 : 0;
     return CRDT_OK;
@@ -3513,28 +3348,6 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     // the sorted path's packed form needs the records' frame: the scan reduces it on the way
     c->segs.from_offsets(batch->offsets, R);
     const bool frame = c->packed_resolve && use_sorted(c, c->segs, R, win_flags);
-    c->last_anchored = false;
-    PackFrame apf;
-    if (frame && !win_flags && !c->counts && batch->mem == CRDT_MEM_DEVICE && !batch->millis && n > 0 && R <= kWindow &&
-        (c->form_off & kFormAnchor) && anchored_frame(c, R, wall, &apf)) {
-        if (c->anchor_skip) {
-            --c->anchor_skip;
-        } else {
-            ev_record(c, kEvStart);
-            st = merge_anchored(c, &dev, wall, apf, out);
-            if (st != kAnchorRetry) {
-                c->last_anchored = true;
-                if (c->timing) {
-                    ev_record(c, kEvEnd);
-                    hipStreamSynchronize(c->stream);
-                }
-                place_finish(c, st >= 0);
-                collect_timing(c);
-                return st;
-            }
-            c->anchor_skip = 16;        // this replica's peers reach below the anchor: exact frames for a while
-        }
-    }
     ev_record(c, kEvStart);
     if ((st = phase_scan(c, &dev, wall, c->d_M.p, true, frame, true, batch->mem == CRDT_MEM_DEVICE))) return st;
     ev_record(c, kEvScan);
@@ -3542,6 +3355,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
     if (!c->resolved && (st = phase_resolve(c, c->d_event.p))) return st;
     ev_record(c, kEvClock);
     st = phase_apply(c, &dev, wall, c->d_event.p, dflags, out, true);
+    if (c->place_k > 1 && c->place_best < 0 && !c->last_sorted && ++c->place_idle >= 2) place_drop(c);
     if (c->timing) {
         ev_record(c, kEvEnd);
         hipStreamSynchronize(c->stream);
@@ -3588,7 +3402,6 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_key8) f |= CRDT_PLAN_KEY8;
         if (c->last_key16) f |= CRDT_PLAN_KEY16;
         if (c->last_hw) f |= CRDT_PLAN_HIGH_WATER;
-        if (c->last_anchored) f |= CRDT_PLAN_ANCHORED;
         if (c->last_flagged) f |= CRDT_PLAN_FLAGGED;
         if (c->last_ordered) f |= CRDT_PLAN_ORDERED;
         if (c->last_combined) f |= CRDT_PLAN_COMBINED;

@@ -127,10 +127,12 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
 void crdt_destroy(crdt_ctx* ctx);
 int crdt_reserve(crdt_ctx* ctx, uint64_t capacity);          /* grow; new rows absent */
 /* Pre-size the sorted path's partition scratch for merges of up to n_records applied records
- * (two partitioned copies, <= 40 B per record), so the first large merge allocates nothing and the
- * buffers are placed while device memory is still unfragmented.  On a single-GPU ctx it also takes the
- * placement tuner's candidate level-1 buffers (CRDT_PLACE_TRIES - 1 more, <= 20 B per record each; freed
- * once the first merges have timed them: crdt_place_info).  Optional. */
+ * (two partitioned copies in the packed form, 27 B per record; a wider form grows them in its first
+ * merge), so the first large merge allocates nothing and the buffers are placed while device memory is
+ * still unfragmented.  On a single-GPU ctx it also asks for the placement tuner's trials
+ * (crdt_place_info): the next sorted merge takes the candidate level-1 buffers, sized for its form
+ * (14 B per record at the fan-in) and together at most 1/8 of the device's HBM; they are freed once
+ * timed, or after two merges that do not take the sorted path.  Optional. */
 int crdt_reserve_scratch(crdt_ctx* ctx, uint64_t n_records);
 /* Row size of the device table: 24 (default) or 32 bytes; the rows are copied over.  24-B rows move
  * 25 % fewer bytes in the sorted path's coalesced passes (many-changeset fan-ins); 32-B rows make
@@ -280,10 +282,8 @@ enum crdt_plan_flags {
     CRDT_PLAN_KEY16 = 32,        /* ... and 14-B level-1 records (2-B key column) */
     CRDT_PLAN_HIGH_WATER = 64,   /* ... and its resolve did not read the rows at or above the table's
                                     high-water mark of written rows (never-written fill) */
-    CRDT_PLAN_ANCHORED = 128,    /* ... on the anchored frame (opt-in, CRDT_SORTED_FORM bit 262144): the
-                                    packed key's lt range fixed before any record is read (every applied
-                                    record is <= max(C_0, wall + 60 s) + R, hlc.dart:92-94), the clock
-                                    scan folded into the level-1 scatter */
+    CRDT_PLAN_ANCHORED = 128,    /* retired in round 5 (the anchored sorted form, measured 0.25 ms slower
+                                    per fan-in step, was removed): never set */
     CRDT_PLAN_WIRE_PACKED = 256, /* sharded ctx: records crossed the all-to-all as 16-B packed
                                     {slot, (lt, rank, changeset) key, val} instead of 20 B */
     CRDT_PLAN_OWN_IN_PLACE = 512, /* sharded ctx: the records this rank owns of its own batch were
@@ -312,8 +312,9 @@ int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [4] */);
 
 /* The level-1 scatter's placement tuner (crdt_merge.hip, PlaceTune; CRDT_PLACE_TRIES, default 3, 1 = off):
- * crdt_reserve_scratch on a single-GPU ctx takes that many candidate level-1 partition buffers; the next
- * sorted-path merges — after one untimed warm-up merge — time the level-1 scatter on each in turn, two
+ * crdt_reserve_scratch on a single-GPU ctx asks for that many candidate level-1 partition buffers (the
+ * warm-up merge takes those that fit in 1/8 of HBM); the next sorted-path merges time the level-1 scatter
+ * on each in turn, two
  * rounds, and keep the fastest (the scatter's time follows where its destination lies in physical memory;
  * DESIGN.md §6).  *n: candidates (0 / 1: no trials); *kept: the kept one (-1 while the trials run); *done:
  * merges the tuner has used (the warm-up, then two per candidate); ms[0 .. 3]: each candidate's level-1

@@ -1058,22 +1058,17 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
     t.close()
 
 
-ANCHOR = 262144           # CRDT_SORTED_FORM bit: the anchored sorted path on (default: the scan pass)
-
-
-@pytest.mark.parametrize("anchored", [True, False])
 @pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536"])
-def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off, anchored):
+def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
     level-2 histogram with 2-B loads into shared bins, the level-1 scatter's / the scan's narrow
-    loads, 32K-record level-2 tiles) gives the same rows, on the anchored path and the scan's."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (ANCHOR if anchored else 0)))
+    loads, 32K-record level-2 tiles) gives the same rows."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
     case = _frame_edge_case(99)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
-    assert res["plan"]["anchored"] == anchored, res["plan"]
     assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
 
 
@@ -1103,23 +1098,21 @@ def _cold_bucket_case(seed):
     return case
 
 
-@pytest.mark.parametrize("anchored", [True, False])
 @pytest.mark.parametrize("form_off", ["0", "64", "128", "256", "448", "512", "1024", "2048", "8192", "32768",
                                       "65536"])
-def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_off, anchored):
+def test_sorted_packed_form_switches_cold_buckets(gpu_device, monkeypatch, form_off):
     """Every CRDT_SORTED_FORM switch on records spread over many cold buckets, two levels: the
     unsplit-bucket resolve of each form (the changed-rows-only writes with 13-B final records
-    among them) against the oracle, anchored and not."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(int(form_off) | (ANCHOR if anchored else 0)))
+    among them) against the oracle."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", form_off)
     case = _cold_bucket_case(131)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=case["n_ids"],
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"], res["plan"]
     assert res["plan"]["key8"] == (form_off not in ("128", "448")), res["plan"]
-    assert res["plan"]["anchored"] == anchored, res["plan"]
 
 
-def _anchor_case(kind):
+def _kind_case(kind):
     if kind == "edges":
         return _frame_edge_case(141), (1 << 20) + 3
     if kind == "late_drift":
@@ -1143,41 +1136,35 @@ def _anchor_case(kind):
 
 
 @pytest.mark.parametrize("kind", ["edges", "late_drift", "dup", "send_overflow", "hot", "cold", "one_level"])
-def test_sorted_anchored(gpu_device, monkeypatch, kind):
-    """The anchored sorted path (the packed key's lt frame fixed from C_0 and the wall clock before
-    any record is read, the clock scan folded into the level-1 scatter, the stop point applied by the
-    resolve): rows, canonical, status and exception fields equal the oracle's, on frame edges,
-    exceptions raised in recv() (a late drift, a duplicate node) and in send(), split hot buckets,
-    cold buckets and one partition level — and the scan's path (the default) gives the same."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(ANCHOR))
-    case, cap = _anchor_case(kind)
+def test_sorted_packed_kinds(gpu_device, kind):
+    """The packed sorted path with a declared rank bound on frame edges, exceptions raised in recv() (a
+    late drift, a duplicate node) and in send(), split hot buckets, cold buckets and one partition level:
+    rows, canonical, status and exception fields equal the oracle's."""
+    case, cap = _kind_case(kind)
     bound = int(case["rank"].max()) + 1
-    kw = dict(path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound, device_cols=True)
-    res = compare_with_oracle(case, **kw)
-    assert res["path"] == "sorted" and res["plan"]["anchored"] and res["plan"]["packed"], res["plan"]
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound,
+                              device_cols=True)
+    assert res["path"] == "sorted" and res["plan"]["packed"], res["plan"]
     if kind in ("late_drift", "dup", "send_overflow"):
         assert res["status"] != 0, res
-    monkeypatch.setenv("CRDT_SORTED_FORM", "0")
-    res0 = compare_with_oracle(case, **kw)
-    assert not res0["plan"]["anchored"]
 
 
-@pytest.mark.parametrize("where", ["applied", "after_stop"])
-def test_sorted_anchored_frame_miss(gpu_device, monkeypatch, where):
-    """A record older than the anchored frame reaches (2^L lt values below max(C_0, wall + 60 s) + R):
-    in an applied changeset the anchored call stores nothing and the library reruns it on the scan's
-    exact frame (plan: not anchored); in a changeset after the stop point (a late drift) it is
-    dropped with that changeset and the anchored result stands.  Both equal the oracle."""
-    monkeypatch.setenv("CRDT_SORTED_FORM", str(ANCHOR))
-    case = _late_drift_case(148)                        # stop = 37 (drift at changeset 37)
-    x = int(case["offsets"][10 if where == "applied" else 41]) + 3
-    case["lt"] = case["lt"].copy()
-    case["lt"][x] = (case["wall"] - (1 << 37)) << 16     # ~4 years behind: below any anchored frame
+@pytest.mark.parametrize("tile", ["16384", "20480"])
+@pytest.mark.parametrize("kind", ["edges", "cold", "late_drift"])
+def test_sorted_odd_level1_tile(gpu_device, monkeypatch, tile, kind):
+    """CRDT_L1_TILE other than the two sizes the scan counts (28672 / 14336) partitions on its
+    own tile boundaries, so the scan's fused histogram must not be used — 20,000-record changesets give
+    two level-1 tiles at 16384 as at 14336, on different boundaries.  Rows vs the oracle."""
+    monkeypatch.setenv("CRDT_L1_TILE", tile)
+    case, cap = _kind_case(kind)
+    if kind == "edges":
+        case = make_case(seed=149, R=70, per_cs=20_000, n_local=300_000, n_new=200_000, millis_span=6,
+                         counter_span=3, n_ranks=11, tomb_frac=0.1)
+        cap = max(case["n_ids"], (1 << 20) + 3)
     bound = int(case["rank"].max()) + 1
-    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
-                              rank_bound=bound, device_cols=True)
-    assert res["status"] == 1 and res["n_stored"] == 37, res
-    assert res["plan"]["anchored"] == (where == "after_stop"), res["plan"]
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=cap, rank_bound=bound,
+                              device_cols=True)
+    assert res["path"] == "sorted" and not res["plan"]["hist_in_scan"], res["plan"]
 
 
 @pytest.mark.parametrize("L", [44, 45, 46, 47])
@@ -1756,15 +1743,12 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
     assert res["path"] == "gather" and not res["plan"]["flagged"]
 
 
-@pytest.mark.parametrize("chk", ["0", "4"])
-@pytest.mark.parametrize("bits", ["1", "0", "2"])
-def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, bits):
-    """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0) and with one per 16 staged
-    bytes (4; the default is one per 64), the flags between the passes as bits (CRDT_FLAG_BITS=1, the
-    default) or bytes: split hot bucket, cold buckets on the 2-B level-1 key column, a late drift —
-    same flags, rows and counts as the oracle."""
+@pytest.mark.parametrize("chk", ["0", "4", "6"])
+def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk):
+    """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0), with one per 16 staged
+    bytes (4) and one per 64 (6, the default): split hot bucket, cold buckets on the 2-B level-1 key
+    column, a late drift — same flags, rows and counts as the oracle."""
     monkeypatch.setenv("CRDT_FBACK_CHK", chk)
-    monkeypatch.setenv("CRDT_FLAG_BITS", bits)
     case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
                      n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
     assert _flagged(case, _TWO)["plan"]["flagged"]
