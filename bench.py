@@ -109,6 +109,26 @@ class GpuSampler:
                 "fields": "[mean, min, max] over the samples inside each timed step (~2 ms apart)"}
 
 
+class Heartbeat:
+    """A line on stderr (rank 0) every `every` seconds while a long phase runs — full-size N > 1 rehearsals
+    (several ranks generating 1B records on one GPU, host-staged exchanges) go minutes between log lines."""
+
+    def __init__(self, every: float = 45.0):
+        import threading
+        self.phase = "start"
+        self.t0 = time.time()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, args=(every,), daemon=True)
+        self._t.start()
+
+    def _run(self, every):
+        while not self._stop.wait(every):
+            log(f"... {self.phase} ({time.time() - self.t0:.0f} s)")
+
+    def stop(self):
+        self._stop.set()
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -177,6 +197,9 @@ def main():
     from crdt_amd.dist import GlooComm, attach_rccl
     from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
 
+    beat = Heartbeat()
+    beat.phase = "creating the table"
+
     def all_max(x: float) -> float:
         if world == 1:
             return x
@@ -199,36 +222,21 @@ def main():
         table.reserve_scratch(args.records if world == 1 else int(args.records / world * 1.25))
         torch.cuda.synchronize()
 
+    beat.phase = "generating the workload"
     t0 = time.time()
     census = args.config == "fanin" and not args.no_census and world > 1      # N > 1: counted at generation
-    if args.config == "fanin":
-        wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
-                       device=dev, order=args.order, rank=rank, world=world, route=world > 1, census=census,
-                       millis_span=args.millis_span)
-        workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
-                    f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
-                    f"{args.order} order), local map 2^{int(np.log2(args.local))} keys")
-        if args.millis_span != 1 << 16:
-            workload += f", clocks over {args.millis_span:,} ms"
-        if world > 1:
-            workload += (f"; replica j arrives whole on rank j % {world}, keys owned by rank key % {world}, "
-                         f"records routed to their owner inside the step (one grouped all-to-all per step)")
-    elif args.config == "cfg2":
-        assert world == 1, "cfg2 is a single-GPU configuration"
-        wl = gen_cfg2(device=dev)
-        workload = "cfg2: 10M-key local map + one 10M-record changeset, ~50% key overlap"
-    elif args.config == "cfg3":
-        assert world == 1, "cfg3 is a single-GPU configuration"
-        wl = gen_cfg3(device=dev)
-        workload = ("cfg3: 100M-key local map, 1024 replicas x 97,657 records, Zipf(1.0) keys, millis over 8 "
-                    "values x counters over 4 (ties decided by node rank)")
-    else:
-        wl = gen_cfg5(device=dev, rank=rank, world=world)
-        workload = ("cfg5 streaming: 100M-key table, 100 deltas x 10M records, one merge call per delta "
-                    "(advancing wall), 10% tombstones, peers 1..16")
-        if world > 1:
-            workload += (f"; every delta split into {world} contiguous parts (part r on rank r), keys owned by "
-                         f"rank key % {world}: one collective merge per delta routes the records to their owners")
+    # gloo rehearsal (several ranks on ONE GPU): the ranks generate their workloads one after another —
+    # heavy kernels of eight processes time-sliced on one GPU took over 18 minutes for the 1B fan-in
+    serial_gen = world > 1 and backend != "nccl"
+    for r_ in range(world if serial_gen else 1):
+        if serial_gen:
+            dist.barrier()
+            log(f"generating rank {r_}'s workload ({time.time() - t0:.0f} s)")
+            if r_ != rank:
+                continue
+        wl, workload = make_workload(args, dev, rank, world, census)
+    if serial_gen:
+        dist.barrier()
     torch.cuda.synchronize()
     log(f"workload generated in {time.time() - t0:.1f}s: {workload}")
 
@@ -317,6 +325,8 @@ def main():
             if sampler:
                 sampler.mark(ts, te)
             step_ms.append(all_max(te - ts) * 1e3)       # max over ranks
+            if world > 1:
+                log(f"timed step {si}: {step_ms[-1]:.1f} ms")
             if ab:
                 ab[2].setdefault(ab[1][si % len(ab[1])], []).append(step_ms[-1])
             tms, table_timing[1] = table_timing[1] or [table.timing()], []
@@ -338,11 +348,14 @@ def main():
     # N > 1 fan-in: the library's routing tuner (comm_path.inc RouteTune) takes its trial calls — each way of
     # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4 and in 1), the fastest kept — before
     # the warmup, so every timed step takes the chosen way
+    beat.phase = "merging"
     route_tune = None
     if world > 1 and args.config == "fanin" and os.environ.get("CRDT_ROUTE_TUNE", "1") != "0":
-        for _ in range(10):
+        for i in range(10):
             reset()
+            ts = time.perf_counter()
             step()
+            log(f"routing tuner call {i}: {(time.perf_counter() - ts) * 1e3:.1f} ms, plan {table.last_plan()}")
             if table.route_tune()["best"] is not None:
                 break
         route_tune = table.route_tune()
@@ -361,9 +374,12 @@ def main():
                 break                                    # (this path does not partition: nothing to time)
         placement = table.place_info()
         log(f"placement tuner: {placement}")
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         reset()
+        ts = time.perf_counter()
         step()
+        if world > 1:
+            log(f"warmup {i}: {(time.perf_counter() - ts) * 1e3:.1f} ms")
     sampler = GpuSampler(local_rank).start()
     step_ms, tsum, res = timed_run(args.steps, sampler)
     gpu_clocks = sampler.stop()
@@ -542,6 +558,7 @@ def main():
         roofline["traffic"] = pm["hbm_bytes_per_step"]
         roofline["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
 
+    beat.phase = "baselines and parity"
     cpu = cpu16 = cpu_omp = parity = None
     if world > 1 and args.config in ("fanin", "cfg5") and not args.no_cpu:
         # N > 1: every rank digests its shard (one 64-bit word per 2^20 slots, after the timed path's
@@ -658,6 +675,7 @@ def main():
                          "apply_launches": launches_per_step,
                          "device_total": round(tsum.get("total_ms", 0) / K, 3)},
     }
+    beat.stop()
     if rank == 0:
         print(json.dumps(out), flush=True)
     table.close()
@@ -666,6 +684,40 @@ def main():
         sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_workload(args, dev, rank, world, census):
+    """The configuration's synthetic workload on this rank (BASELINE.json configs; crdt_amd/workload.py)."""
+    from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
+    if args.config == "fanin":
+        wl = gen_fanin(total=args.records, R=args.replicas, K=args.keys, n_local=args.local, s=args.zipf,
+                       device=dev, order=args.order, rank=rank, world=world, route=world > 1, census=census,
+                       millis_span=args.millis_span)
+        workload = (f"fanin: {wl['total']:,} records = {wl['R']} replicas x {wl['n_per_replica']:,}, "
+                    f"Zipf({args.zipf}) keys over 2^{int(np.log2(args.keys))} ids (unique per replica, "
+                    f"{args.order} order), local map 2^{int(np.log2(args.local))} keys")
+        if args.millis_span != 1 << 16:
+            workload += f", clocks over {args.millis_span:,} ms"
+        if world > 1:
+            workload += (f"; replica j arrives whole on rank j % {world}, keys owned by rank key % {world}, "
+                         f"records routed to their owner inside the step (one grouped all-to-all per step)")
+    elif args.config == "cfg2":
+        assert world == 1, "cfg2 is a single-GPU configuration"
+        wl = gen_cfg2(device=dev)
+        workload = "cfg2: 10M-key local map + one 10M-record changeset, ~50% key overlap"
+    elif args.config == "cfg3":
+        assert world == 1, "cfg3 is a single-GPU configuration"
+        wl = gen_cfg3(device=dev)
+        workload = ("cfg3: 100M-key local map, 1024 replicas x 97,657 records, Zipf(1.0) keys, millis over 8 "
+                    "values x counters over 4 (ties decided by node rank)")
+    else:
+        wl = gen_cfg5(device=dev, rank=rank, world=world)
+        workload = ("cfg5 streaming: 100M-key table, 100 deltas x 10M records, one merge call per delta "
+                    "(advancing wall), 10% tombstones, peers 1..16")
+        if world > 1:
+            workload += (f"; every delta split into {world} contiguous parts (part r on rank r), keys owned by "
+                         f"rank key % {world}: one collective merge per delta routes the records to their owners")
+    return wl, workload
 
 
 def pmc_profile(args, path, world):

@@ -2937,6 +2937,10 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_L1_TILE"))
         c->l1_tile = std::min<uint32_t>((uint32_t)std::max(atoi(e), 0) / 1024u * 1024u, (uint32_t)kPTile);
     if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
+    if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
+        const int v = atoi(e);
+        c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+    }
     c->fail_rank = -1;
     c->fail_at = 0;
     if (const char* e = getenv("CRDT_TEST_FAIL")) {     // "rank:point" (comm_path.inc, kFail*)
@@ -2966,10 +2970,6 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
-    }
-    if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
-        const int v = atoi(e);
-        c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_misc, sizeof(Misc)) != hipSuccess ||

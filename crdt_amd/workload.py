@@ -77,9 +77,15 @@ def gen_fanin(total: int = 1_000_000_000, R: int = 1024, K: int = 1 << 28, n_loc
             seen[kk // world] = True
             del kk
         if order == "shuffled":
-            perm = torch.argsort(torch.rand(rows, n, device=dev, generator=gen), dim=1)
-            key = torch.gather(key, 1, perm)
-            del perm
+            rnd = torch.rand(rows, n, device=dev, generator=gen)
+            if route and world > 1:                      # only this rank's home replicas are kept: shuffle
+                hr = [r_ for r_ in range(rows) if (j0 + r_) % world == rank]     # those (same draws)
+                if hr:
+                    hi = torch.tensor(hr, device=dev)
+                    key[hi] = torch.gather(key[hi], 1, torch.argsort(rnd[hi], dim=1))
+            else:
+                key = torch.gather(key, 1, torch.argsort(rnd, dim=1))
+            del rnd
         ms = BASE_MILLIS + torch.randint(0, millis_span, (rows, n), device=dev, generator=gen)
         cnt = torch.randint(0, counter_span, (rows, n), device=dev, generator=gen)
         lt = (ms << 16) + cnt

@@ -205,6 +205,13 @@ int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint
  *   6. SUM all-reduce of the per-record counts and of the key-range error.
  * Every rank returns the same status, stop point, canonical and counts; win_flags
  * (optional, [n] of the local batch) come back to the rank that passed the record.
+ * A failure local to one rank (CRDT_E_NOMEM, CRDT_E_INVALID of its own batch, CRDT_E_HIP)
+ * is carried through the call's collectives and returned by EVERY rank — no rank is left
+ * waiting in a collective its peers will not post.  Before the record exchange nothing is
+ * stored and the canonical clock does not move; a failure in the owners' apply (after the
+ * exchange) leaves the other ranks' rows of the stopped call stored and the canonical
+ * unchanged (re-merging the same batch is exact).  Rank-local still: a failing transport
+ * (CRDT_E_COMM) and a rank that cannot allocate the call's O(R) gather words.
  * Keys in the batch are GLOBAL key ids, unless crdt_set_presharded(ctx, 1): then every
  * record is already on its owner and key_id holds its slot (no record exchange).
  *
