@@ -346,12 +346,13 @@ def main():
         return step_ms, tsum, res
 
     # N > 1 fan-in: the library's routing tuner (comm_path.inc RouteTune) takes its trial calls — each way of
-    # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4 and in 1), the fastest kept — before
+    # moving the records twice (route_l1 in 2 pieces, the combine, route_l1 in 4 and in 1, route_l1 with the head
+    # fold), the fastest kept — before
     # the warmup, so every timed step takes the chosen way
     beat.phase = "merging"
     route_tune = None
     if world > 1 and args.config == "fanin" and os.environ.get("CRDT_ROUTE_TUNE", "1") != "0":
-        for i in range(10):
+        for i in range(12):
             reset()
             ts = time.perf_counter()
             step()
@@ -587,13 +588,15 @@ def main():
     # ---- N > 1: one timed step in each way of moving the records (the same job; CRDT_ENV_DYNAMIC):
     # route_l1 = home records partitioned straight into the owners' level-1 buckets (14-B level-1
     # records over the exchange, owners from level 2 on), combine = the map-side fold first (16-B
-    # packed maxima), route = plain record routing (owners run the whole sorted path); DESIGN §7
+    # packed maxima), route = plain record routing (owners run the whole sorted path), route_l1_head = route_l1
+    # with every owner's first level-1 digit folded at the sender; DESIGN §7
     route_ab = None
     if world > 1 and args.config == "fanin":
         route_ab = {"default_plan": {k: v for k, v in plan.items()
-                                     if k in ("route_l1", "combined", "wire_packed", "rl1_pieces")}}
+                                     if k in ("route_l1", "combined", "wire_packed", "rl1_pieces", "rl1_head")}}
         modes = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1"},
                  "route_l1_4": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
+                 "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2"},
                  "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
                  "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"}}
         saved = {k: os.environ.get(k) for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_RL1_SPLIT")}
@@ -608,7 +611,8 @@ def main():
             p5 = table.last_plan()
             assert r5["status"] == 0 and r5["canonical_lt"] == res["canonical_lt"], (name, r5, res)
             route_ab[name] = {"ms": round(ms5, 3), "value": round(total_records / (ms5 / 1e3), 1),
-                              "route_l1": p5["route_l1"], "combined": p5["combined"], "rl1_pieces": p5["rl1_pieces"]}
+                              "route_l1": p5["route_l1"], "combined": p5["combined"], "rl1_pieces": p5["rl1_pieces"],
+                              "rl1_head": p5["rl1_head"]}
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)

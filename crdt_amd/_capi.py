@@ -74,7 +74,7 @@ class CrdtCommOps(ctypes.Structure):
 
 
 COMM_ID_BYTES = 128
-ABI_VERSION = 3                            # include/crdt_merge.h CRDT_ABI_VERSION
+ABI_VERSION = 4                            # include/crdt_merge.h CRDT_ABI_VERSION
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32

@@ -1494,6 +1494,8 @@ struct Rl1Scratch {
     HBuf<uint64_t> hplan;
     size_t pw = 0, u32w = 0;        // the plan's words (rl1_owner_prep)
     uint32_t nt2 = 0, nc2 = 0;      // level-2 tiles and scan chunks
+    uint32_t ngrp = 0;              // level-1 buckets (groups of segments) level 2 partitions
+    size_t nsg = 0;                 // ... and their segments
     uint64_t nw = 0;                // records of the piece at this owner
     void release() {
         hist.release(); toff.release(); part.release(); choff.release(); dstart2.release(); tseg.release();
@@ -1648,7 +1650,11 @@ struct crdt_ctx {
                                     // 0 off, 1 auto = from 64 changesets, 2 always)
     bool last_combined = false;
     uint32_t sparse_t = 2048;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
-    bool route_l1 = true;           // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition
+    int route_l1 = 1;               // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition;
+                                    // 2: route_l1 always with the sender-side fold of the owners' first digit
+    bool rl1_call_head = false;     // this call's route_l1 folds the owners' first level-1 digit (the Zipf head)
+    bool last_rl1_head = false;     // ... the last routed merge's did
+    uint64_t last_rl1_head_in = 0, last_rl1_head_out = 0;   // ... its head records before / after the fold
     uint32_t rl1_pieces = 2;        // CRDT_RL1_SPLIT: route_l1's pipelined pieces (0 / 1: one; up to kRl1MaxPieces)
     uint32_t rl1_call_pieces = 2;   // ... this call's (the tuner's way 2 takes kRl1MaxPieces)
     uint32_t last_rl1_pieces = 0;   // ... the last routed merge's
@@ -1660,9 +1666,9 @@ struct crdt_ctx {
     struct RouteTune {
         uint64_t shape = 0;         // (R, G, cap) the trials were taken for
         uint32_t trial = 0;         // trial calls taken (kTrials per way)
-        int best = -1;              // 0 route_l1 in 2 pieces, 1 combine, 2 route_l1 in 4, 3 route_l1 in 1;
-                                    // -1 while the trials run
-        long long us[4] = {-1, -1, -1, -1};   // each way's second call, max over ranks (microseconds)
+        int best = -1;              // 0 route_l1 in 2 pieces, 1 combine, 2 route_l1 in 4, 3 route_l1 in 1,
+                                    // 4 route_l1 in 2 pieces with the head fold; -1 while the trials run
+        long long us[5] = {-1, -1, -1, -1, -1};   // each way's second call, max over ranks (microseconds)
     } rt;
     int tune_mode = -1;             // this call's way from the tuner (-1: the fixed rule)
     bool tune_trial = false;        // ... and the call took it with both ways open (a trial / a tuned call)
@@ -1671,7 +1677,13 @@ struct crdt_ctx {
     DBuf<uint32_t> rl_rec;          // route_l1: 12-B level-1 payloads, send area [0, n) then the receive area
     DBuf<uint16_t> rl_k16;          // ... and their 2-B key columns
     uint64_t rl_cap = 0;            // records both hold
-    Rl1Scratch rl_os[kRl1MaxPieces];   // the owner's level 2 + resolve of each piece
+    Rl1Scratch rl_os[kRl1MaxPieces + 1];   // the owner's level 2 + resolve of each piece (+ the folded head)
+    Rl1Scratch rl_hf;               // route_l1's head fold at the sender: level 2 + the emitting resolve
+    DBuf<uint32_t> rl_hrec;         // ... the folded head records bound for the peers: 12-B payloads
+    DBuf<uint16_t> rl_hk16;         // ... and 2-B key columns
+    DBuf<unsigned long long> rl_hcnt;   // ... [G] sent, [G] received, [1] own, [G] bases
+    HBuf<unsigned long long> h_hcnt;
+    hipEvent_t rl_evh = nullptr;    // ... the fold is done (side stream)
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
@@ -2925,7 +2937,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
-    if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("CRDT_RL1_SPLIT")) {   // 0: one piece, 1: two (the default), n: n pieces
         const int v = atoi(e);
         c->rl1_pieces = std::min<uint32_t>(v <= 0 ? 1u : v == 1 ? 2u : (uint32_t)v, kRl1MaxPieces);
@@ -2999,6 +3011,7 @@ void crdt_destroy(crdt_ctx* c) {
     for (hipEvent_t e : c->rl_evs) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->rl_evx) if (e) hipEventDestroy(e);
     if (c->rl_evo) hipEventDestroy(c->rl_evo);
+    if (c->rl_evh) hipEventDestroy(c->rl_evh);
     if (c->sstream) hipStreamDestroy(c->sstream);
     if (c->ostream) hipStreamDestroy(c->ostream);
     if (c->table.base) hipFree(c->table.base);
@@ -3028,6 +3041,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->e_icnt.release(); c->e_off.release(); c->e_csum.release(); c->e_bbase.release();
     c->h_ebase.release();
     c->rl_rec.release(); c->rl_k16.release(); for (Rl1Scratch& os : c->rl_os) os.release();
+    c->rl_hf.release(); c->rl_hrec.release(); c->rl_hk16.release(); c->rl_hcnt.release(); c->h_hcnt.release();
     for (hipEvent_t e : c->events) hipEventDestroy(e);
     for (hipEvent_t e : c->cevents) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
@@ -3411,6 +3425,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;
     if (c->tune_trial) f |= CRDT_PLAN_ROUTE_TUNED;
     if (c->last_route_l1) f |= (c->last_rl1_pieces & 7u) << CRDT_PLAN_RL1_PIECES_SHIFT;
+    if (c->last_route_l1 && c->last_rl1_head) f |= CRDT_PLAN_RL1_HEAD;
     *flags = f;
     return CRDT_OK;
 }
@@ -3427,7 +3442,7 @@ int crdt_place_info(const crdt_ctx* c, int32_t* n, int32_t* kept, int32_t* done,
 int crdt_route_tune_info(const crdt_ctx* c, int32_t* best, int64_t* us) {
     if (!c || !best || !us) return CRDT_E_INVALID;
     *best = c->rt.best;
-    for (int w = 0; w < 4; ++w) us[w] = c->rt.us[w];
+    for (int w = 0; w < 5; ++w) us[w] = c->rt.us[w];
     return CRDT_OK;
 }
 

@@ -312,7 +312,7 @@ class DeviceTable:
     PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32,
                   "high_water": 64, "anchored": 128, "wire_packed": 256, "own_in_place": 512,
                   "flagged": 1024, "ordered": 2048,
-                  "combined": 4096, "route_l1": 8192, "route_tuned": 16384}
+                  "combined": 4096, "route_l1": 8192, "route_tuned": 16384, "rl1_head": 262144}
 
     def last_plan(self) -> dict:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""
@@ -333,16 +333,17 @@ class DeviceTable:
         return {"candidates": n.value, "kept": kept.value if kept.value >= 0 else None, "merges_used": done.value,
                 "level1_ms": [round(float(m), 3) for m in ms[:max(n.value, 0)]]}
 
-    TUNE_WAYS = ("route_l1", "combine", "route_l1_4", "route_l1_1")
+    TUNE_WAYS = ("route_l1", "combine", "route_l1_4", "route_l1_1", "route_l1_head")
 
     def route_tune(self) -> dict:
         """crdt_route_tune_info: the sharded fan-in routing the ctx measured ({'best': None while the
-        trials run, else 'route_l1' (2 pipelined pieces) / 'combine' / 'route_l1_4' (4) / 'route_l1_1' (1);
-        '<way>_ms': each way's timed call, max over ranks, None if not yet})."""
+        trials run, else 'route_l1' (2 pipelined pieces) / 'combine' / 'route_l1_4' (4) / 'route_l1_1' (1) /
+        'route_l1_head' (2 pieces, the owners' first digit folded at the sender); '<way>_ms': each way's timed
+        call, max over ranks, None if not yet})."""
         best = ctypes.c_int32(0)
-        us = (ctypes.c_int64 * 4)()
+        us = (ctypes.c_int64 * 5)()
         self._check(self._lib.crdt_route_tune_info(self._ctx, ctypes.byref(best), us), "crdt_route_tune_info")
-        out = {"best": self.TUNE_WAYS[best.value] if 0 <= best.value < 4 else None}
+        out = {"best": self.TUNE_WAYS[best.value] if 0 <= best.value < len(self.TUNE_WAYS) else None}
         for w, u in zip(self.TUNE_WAYS, us):
             out[f"{w}_ms"] = u / 1e3 if u >= 0 else None
         return out

@@ -99,7 +99,7 @@ typedef _CtxOnlyD = int Function(Pointer<Void>);
 
 const int crdtCommIdBytes = 128;
 /// include/crdt_merge.h CRDT_ABI_VERSION: the struct layouts above are this version's.
-const int crdtAbiVersion = 3;
+const int crdtAbiVersion = 4;
 typedef _AbiC = Int32 Function();
 typedef _AbiD = int Function();
 

@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define CRDT_ABI_VERSION 3          /* 3: crdt_timing gained part1_records (round 3) */
+#define CRDT_ABI_VERSION 4          /* 3: crdt_timing gained part1_records (round 3); 4: crdt_route_tune_info
+                                       reports five ways (round 5) */
 #define CRDT_NULL_VALUE 0xFFFFFFFFu
 
 /* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
@@ -305,7 +306,10 @@ enum crdt_plan_flags {
                                     owners started at level 2 (comm_path.inc, route_l1) */
     CRDT_PLAN_ROUTE_TUNED = 16384, /* sharded ctx: the way (route_l1 or the combine) came from the routing
                                     tuner, a trial or its measured choice (crdt_route_tune_info) */
-    CRDT_PLAN_RL1_PIECES_SHIFT = 15 /* bits 15-17: route_l1's pipelined pieces (1-4; 0: not route_l1) */
+    CRDT_PLAN_RL1_PIECES_SHIFT = 15, /* bits 15-17: route_l1's pipelined pieces (1-4; 0: not route_l1) */
+    CRDT_PLAN_RL1_HEAD = 262144  /* route_l1 folded each owner's first level-1 digit (its 2^20 lowest slots,
+                                    the Zipf head) at the sender: one packed maximum per key crossed the
+                                    exchange for those keys (comm_path.inc) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 
@@ -314,9 +318,9 @@ int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
  * way twice, the second call of each timed on the host and MAX-reduced over the ranks; later calls with the
  * same (changesets, ranks, capacity) take the fastest.  *best: -1 while the trials run (or before any such
  * call), 0 = route_l1 in 2 pipelined pieces, 1 = the map-side combine, 2 = route_l1 in 4 pieces,
- * 3 = route_l1 in one; us[0 .. 3]: their timed calls in microseconds (-1: not yet).  Every way leaves the
- * same rows. */
-int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [4] */);
+ * 3 = route_l1 in one, 4 = route_l1 in 2 pieces with the head fold (CRDT_PLAN_RL1_HEAD); us[0 .. 4]: their
+ * timed calls in microseconds (-1: not yet).  Every way leaves the same rows. */
+int crdt_route_tune_info(const crdt_ctx* ctx, int32_t* best, int64_t* us /* [5] */);
 
 /* The level-1 scatter's placement tuner (crdt_merge.hip, PlaceTune; CRDT_PLACE_TRIES, default 3, 1 = off):
  * crdt_reserve_scratch on a single-GPU ctx asks for that many candidate level-1 partition buffers (the

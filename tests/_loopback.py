@@ -24,6 +24,7 @@ class LoopbackComm:
         self.G = G
         self.error = None
         self.evs = []                                  # (start, end) events around each record exchange
+        self.sent = 0                                  # bytes rank 0 sent its peers (all exchanges)
 
     def _event(self):
         e = ctypes.c_void_p()
@@ -38,6 +39,10 @@ class LoopbackComm:
             tot += ms.value
         self.evs = []
         return tot
+
+    def exchange_bytes(self):
+        b, self.sent = self.sent, 0
+        return b
 
     def ops(self):
         G = self
@@ -60,7 +65,9 @@ class LoopbackComm:
             return 0
 
         def _a2a(user, n_cols, send, recv, eb, sc, sd, rc, rd, stream):
-            big = sum(sc[d] * eb[k] for d in range(G.G) for k in range(n_cols)) > (1 << 20)
+            nbytes = sum(sc[d] * eb[k] for d in range(G.G) for k in range(n_cols))
+            G.sent += nbytes
+            big = nbytes > (1 << 20)
             if big:
                 a, b = G._event(), G._event()
                 hip.hipEventRecord(a, stream)

@@ -76,6 +76,6 @@ def test_bench_two_ranks_routed(gpu_device):
     assert ab["combine"]["combined"] and not ab["route"]["route_l1"] and not ab["route"]["combined"]
     assert all(ab[m]["ms"] > 0 for m in ("route_l1", "combine", "route"))
     tune = d["route_tune"]                                      # the way every timed step took, measured
-    ways = ("route_l1", "combine", "route_l1_4", "route_l1_1")
+    ways = ("route_l1", "combine", "route_l1_4", "route_l1_1", "route_l1_head")
     assert tune["best"] in ways and all(tune[f"{w}_ms"] > 0 for w in ways)
     assert ab["default_plan"]["combined"] == (tune["best"] == "combine")

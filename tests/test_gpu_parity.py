@@ -568,13 +568,15 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R, calls=1):
 
 
 @pytest.mark.parametrize("combine,route_l1,split", [("1", "1", "1"), ("0", "1", "1"), ("0", "1", "0"), ("0", "1", "4"),
-                                                    ("0", "1", "3"), ("0", "0", "1")])
+                                                    ("0", "1", "3"), ("0", "0", "1"), ("0", "2", "1"), ("0", "2", "0"),
+                                                    ("0", "2", "4")])
 def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1, split):
     """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
     routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
     map-side combine (each rank folds its home records per key before the exchange), with the routed
     level-1 partition (home records partitioned straight into the owners' level-1 buckets, owners from
-    level 2 on), and with plain record routing."""
+    level 2 on; route_l1 = 2: with every owner's first level-1 digit folded at the sender, one packed maximum
+    per key, sent after the pieces), and with plain record routing."""
     monkeypatch.setenv("CRDT_COMBINE", combine)
     monkeypatch.setenv("CRDT_ROUTE_L1", route_l1)
     monkeypatch.setenv("CRDT_RL1_SPLIT", split)             # route_l1 in two pipelined pieces / in one
@@ -609,7 +611,8 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
     for rank, res, path, shard, plan in outs:
         assert path == "sorted"
         assert plan["combined"] == (combine == "1"), plan
-        assert plan["route_l1"] == (combine == "0" and route_l1 == "1"), plan
+        assert plan["route_l1"] == (combine == "0" and route_l1 != "0"), plan
+        assert plan["rl1_head"] == (plan["route_l1"] and route_l1 == "2"), plan
         if plan["route_l1"]:                                   # pieces cut at changeset boundaries
             assert plan["rl1_pieces"] == {"0": 1, "1": 2}.get(split, int(split)), plan
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
@@ -664,8 +667,8 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
     collectives, so the partition, the exchanges and the owners' work overlap on their three streams as
     they do on the node — on one GPU through a loopback communicator (tests/_loopback.py: rank 0 of G ranks
     that all hold its data; the peers' parts come back as device copies).  route_l1 in 1, 2, 3 and 4
-    pipelined pieces, record routing and the map-side fold apply the same records and must leave the same
-    rows.  (Under the loopback, keys of different owners share rank 0's slots, so two records of one slot
+    pipelined pieces (and in 2 and 1 with the head fold), record routing and the map-side fold apply the same
+    records and must leave the same rows.  (Under the loopback, keys of different owners share rank 0's slots, so two records of one slot
     may carry equal packed keys and the order-free fold may keep either value: lt / rank / mod must match
     exactly, val in all but a handful of such tie slots.)"""
     from crdt_amd import DeviceTable
@@ -680,7 +683,8 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
     comm = LoopbackComm(G)
     t.comm_init_ops(G, 0, comm)
     ways = {"1": ("0", "1", "0", 1), "2": ("0", "1", "1", 2), "3": ("0", "1", "3", 3), "4": ("0", "1", "4", 4),
-            "route": ("0", "0", "1", 0), "fold": ("2", "1", "1", 0)}
+            "route": ("0", "0", "1", 0), "fold": ("2", "1", "1", 0), "head": ("0", "2", "1", 2),
+            "head1": ("0", "2", "0", 1)}
     rows = {}
     for name, (comb, rl1, split, pieces) in ways.items():
         monkeypatch.setenv("CRDT_COMBINE", comb)
@@ -696,6 +700,7 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
             plan = t.last_plan()
             assert plan["route_l1"] == (pieces > 0) and plan["rl1_pieces"] == pieces, (name, plan)
             assert plan["combined"] == (name == "fold"), (name, plan)
+            assert plan["rl1_head"] == name.startswith("head"), (name, plan)
             rows.setdefault(name, []).append(t.read_rows(np.arange(cap, dtype=np.uint32)))
     comm.exchange_ms()
     t.close()
@@ -726,7 +731,8 @@ def _fanin_reference(K, total, R):
 
 def test_two_rank_route_tune(gpu_device, monkeypatch):
     """The routing tuner (comm_path.inc RouteTune, the auto settings): the first calls take route_l1 in two
-    pieces twice, the map-side combine twice, route_l1 in four pieces and in one twice each, every later call the way
+    pieces twice, the map-side combine twice, route_l1 in four pieces, in one and in two with the head fold twice
+    each, every later call the way
     whose timed call was fastest (max over the ranks, the same way on both ranks); every call leaves
     exactly the unsharded merge's rows."""
     for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_ROUTE_TUNE", "CRDT_RL1_SPLIT"):
@@ -739,7 +745,7 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 10)) for r in range(2)]
+    procs = [ctx.Process(target=_fanin_shard_worker, args=(r, 2, port, q, K, total, R, 12)) for r in range(2)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
@@ -749,14 +755,15 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     tunes = [o[2] for o in outs]
     assert tunes[0] == tunes[1], tunes                        # one decision, from the max over ranks
     tune = tunes[0]
-    ways = ("route_l1", "combine", "route_l1_4", "route_l1_1")
+    ways = ("route_l1", "combine", "route_l1_4", "route_l1_1", "route_l1_head")
     assert tune["best"] in ways and all(tune[f"{w}_ms"] > 0 for w in ways), tune
     assert tune["best"] == min(ways, key=lambda w: tune[f"{w}_ms"]), tune
     for rank, got, _ in outs:
         for i, (res, path, shard, plan) in enumerate(got):
             assert path == "sorted" and plan["route_tuned"], (rank, i, plan)
-            way = tune["best"] if i >= 8 else ways[i // 2]
+            way = tune["best"] if i >= 10 else ways[i // 2]
             assert plan["combined"] == (way == "combine") and plan["route_l1"] == (way != "combine"), (rank, i, plan)
+            assert plan["rl1_head"] == (way == "route_l1_head"), (rank, i, plan)
             if way != "combine":
                 assert plan["rl1_pieces"] == {"route_l1_4": 4, "route_l1_1": 1}.get(way, 2), (rank, i, plan)
             for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
@@ -797,19 +804,23 @@ def test_eight_rank_routed_packed_sorted(gpu_device, monkeypatch, inject, combin
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
 
 
+@pytest.mark.parametrize("head", ["1", "2"])
 @pytest.mark.parametrize("inject", [None, "drift", "dup"])
-def test_eight_rank_route_l1(gpu_device, inject):
+def test_eight_rank_route_l1(gpu_device, monkeypatch, inject, head):
     """The routed level-1 partition at G = 8 (comm_path.inc, route_l1): shards of > 2^20 slots (two
     digits per owner), 16M records in 64 changesets, every rank partitioning its home records straight
     into the 8 owners' level-1 buckets (14-B records over the exchange, own part in place), the owners
     from level 2 on; a drift or duplicate-node record at (41, 123,456).  Every row of all 8 shards,
-    canonical, status and exception fields vs the C oracle, on two calls per ctx (buffers reused)."""
+    canonical, status and exception fields vs the C oracle, on two calls per ctx (buffers reused).
+    head = 2: every owner's first level-1 digit folded at the sender (CRDT_ROUTE_L1=2)."""
+    monkeypatch.setenv("CRDT_ROUTE_L1", head)
     kw = dict(seed=818, R=64, per_cs=250_000, n_local=6_000_000, n_new=3_000_000, millis_span=1 << 12,
               counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
     outs = run_shard_gpu(kw, 8, "routed", path="sorted", counts=False, again=True)
     for rank, res, *_ in outs:
         assert res["path"] == "sorted" and res["plan"]["route_l1"], (rank, res["plan"])
         assert not res["plan"]["combined"], (rank, res["plan"])
+        assert res["plan"]["rl1_head"] == (head == "2"), (rank, res["plan"])
         assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
         if inject:
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res

@@ -15,6 +15,25 @@ case "${STAGE:-check}" in
     timeout -k 10 420 python -u bench.py --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,2097152 --no-cpu --no-census \
       --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_persist.json 2> gpurun_out/${TAG}_ab_persist.log
     rc=$?; grep "A/B\|placement" gpurun_out/${TAG}_ab_persist.log; exit $rc ;;
+  cfg5pmc)
+    # cfg5 (100 streaming 10M-record merges on K2): k_apply's HBM bytes per launch (FETCH_SIZE, WRITE_SIZE in
+    # separate passes), then records per thread of K2 in one process (CRDT_APPLY_ITEMS A/B)
+    ARGS="--config cfg5 --path gather --steps 1 --warmup 0 --no-cpu --no-census --no-pcie --flag-steps 0" MERGES=1 \
+      PMC_PATH=gather PMC_OUT=${TAG}_pmc_cfg5.json bash tools/gpu_pmc_bench.sh || exit $?
+    timeout -k 10 420 python -u bench.py --config cfg5 --path gather --steps 3 --warmup 1 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 --ab CRDT_APPLY_ITEMS=0,1,2,4,8 > gpurun_out/${TAG}_cfg5_items.json \
+      2> gpurun_out/${TAG}_cfg5_items.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_cfg5_items.log; exit $rc ;;
+  cfg3trace)
+    # cfg3's per-merge timeline: device-busy time vs the merge's span (launch gaps), anchor = the clock scan
+    rm -rf gpurun_out/${TAG}_prof_cfg3
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg3 -o run \
+      -- python3 bench.py --config cfg3 --steps 5 --warmup 2 --no-cpu --no-pcie --no-census --flag-steps 0 \
+      > gpurun_out/${TAG}_prof_cfg3.json 2> gpurun_out/${TAG}_prof_cfg3.log
+    rc=$?; echo "[prof] exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_cfg3.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
+    STOP_AT="fill|Fill|k_put_rows" python3 tools/ktrace_calls.py "$k" k_scan > gpurun_out/${TAG}_cfg3_calls.txt; cat gpurun_out/${TAG}_cfg3_calls.txt
+    python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt ;;
   ab)
     timeout -k 10 420 python -u bench.py --steps ${STEPS:-8} --warmup 2 --ab "$AB" --no-cpu --no-census --no-pcie \
       --flag-steps 0 ${ARGS:-} > gpurun_out/${TAG}_ab.json 2> gpurun_out/${TAG}_ab.log

@@ -5,8 +5,10 @@ call; prints, as medians over the calls, each kernel's duration, the device-busy
 (anchor start to next anchor start) and the idle time inside it.  With a HIP API trace beside it
 (rocprofv3 --hip-trace), also the median count and time of each host API per call.
 
-usage: tools/ktrace_calls.py <run_kernel_trace.csv> [anchor substring] [run_hip_api_trace.csv]"""
+usage: tools/ktrace_calls.py <run_kernel_trace.csv> [anchor substring] [run_hip_api_trace.csv]
+STOP_AT=<substring>[|<substring>...]: a call ends at its last kernel before the first launch matching it (span = busy + gaps)."""
 import csv
+import os
 import statistics
 import sys
 from collections import defaultdict
@@ -25,8 +27,14 @@ def main():
     starts = [x[0] for x in anc if x[3] == gmax]
     per = defaultdict(list)
     busy, span, idle, nk = [], [], [], []
+    stop = os.environ.get("STOP_AT")                     # e.g. k_put_rows: the bench's table reset ends a call
     for a, b in zip(starts, starts[1:]):
         ks = [x for x in rows if a <= x[0] < b]
+        if stop:
+            cut = [x[0] for x in ks if any(t in x[2] for t in stop.split("|"))]
+            if cut:
+                ks = [x for x in ks if x[0] < cut[0]]
+            b = max(x[1] for x in ks)
         dur = defaultdict(float)
         for s, e, n, _ in ks:
             dur[n] += (e - s) / 1e3

@@ -28,13 +28,14 @@ from tests._loopback import LoopbackComm  # noqa: E402
 
 N = int(os.environ.get("N", "8"))
 STEPS = int(os.environ.get("STEPS", "3"))
-MODES = os.environ.get("MODES", "route_l1,route_l1_1piece,route_l1_4piece,route,combine").split(",")
+MODES = os.environ.get("MODES", "route_l1,route_l1_head,route_l1_1piece,route_l1_4piece,route,combine").split(",")
 os.environ["CRDT_ENV_DYNAMIC"] = "1"
 ENV = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "1"},
        "route_l1_1piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "0"},
        "route_l1_4piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
        "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"},
-       "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"}}
+       "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
+       "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2", "CRDT_RL1_SPLIT": "1"}}
 
 wl = gen_fanin(total=1_000_000_512, R=1024, K=1 << 28, n_local=1 << 27, s=0.8, device="cuda", rank=0, world=N,
                route=True)
@@ -62,22 +63,25 @@ for it in range(STEPS + 1):
         torch.cuda.synchronize()
         wall_ms = (time.perf_counter() - ts) * 1e3
         xms = comm.exchange_ms()
+        xgb = comm.exchange_bytes() / 1e9
         tm = t.timing()
         plan = t.last_plan()
-        line = (f"{m:9s} step {it}: wall {wall_ms:.2f} ms, device {tm['total_ms']:.2f}, exchange copy {xms:.2f}, "
+        line = (f"{m:9s} step {it}: wall {wall_ms:.2f} ms, device {tm['total_ms']:.2f}, exchange copy {xms:.2f} "
+                f"({xgb:.3f} GB sent), "
                 f"local {tm['total_ms'] - xms:.2f} | scan {tm['scan_ms']:.2f} clock {tm['clock_ms']:.2f} "
                 f"route {tm['route_ms']:.2f} L1 {tm['part1_ms']:.2f} L2 {tm['part2_ms']:.2f} "
-                f"resolve {tm['resolve_ms']:.2f} | route_l1 {plan['route_l1']} combined {plan['combined']} "
+                f"resolve {tm['resolve_ms']:.2f} | route_l1 {plan['route_l1']} head {plan['rl1_head']} "
+                f"combined {plan['combined']} "
                 f"status {res['status']}")
         print(line, flush=True)
         if it > 0:
-            res_t[m].append((tm["total_ms"], xms))
+            res_t[m].append((tm["total_ms"], xms, xgb))
         if it == STEPS:
             rows[m] = t.read_rows(np.arange(cap, dtype=np.uint32))
 for m in MODES:
     v = np.array(res_t[m])
     print(f"mean {m}: device {v[:, 0].mean():.2f} ms, exchange copy {v[:, 1].mean():.2f} ms, "
-          f"local work {(v[:, 0] - v[:, 1]).mean():.2f} ms", flush=True)
+          f"local work {(v[:, 0] - v[:, 1]).mean():.2f} ms, sent {v[:, 2].mean():.3f} GB", flush=True)
 ref = MODES[0]
 for m in MODES[1:]:
     a, b = rows[ref], rows[m]
