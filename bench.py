@@ -594,9 +594,9 @@ def main():
     if world > 1 and args.config == "fanin":
         route_ab = {"default_plan": {k: v for k, v in plan.items()
                                      if k in ("route_l1", "combined", "wire_packed", "rl1_pieces", "rl1_head")}}
-        modes = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1"},
+        modes = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "1"},
                  "route_l1_4": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
-                 "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2"},
+                 "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2", "CRDT_RL1_SPLIT": "1"},
                  "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
                  "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"}}
         saved = {k: os.environ.get(k) for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_RL1_SPLIT")}
