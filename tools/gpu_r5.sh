@@ -34,6 +34,19 @@ case "${STAGE:-check}" in
     k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
     STOP_AT="fill|Fill|k_put_rows" python3 tools/ktrace_calls.py "$k" k_scan > gpurun_out/${TAG}_cfg3_calls.txt; cat gpurun_out/${TAG}_cfg3_calls.txt
     python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt ;;
+  final)
+    # the round's default bench line, its kernel trace (--stats) and its PMC traffic, then the scatters' SQ counters
+    timeout -k 10 420 python -u bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
+    rc=$?; tail -3 gpurun_out/${TAG}_bench_default.log; [ $rc -eq 0 ] || exit $rc
+    rm -rf gpurun_out/${TAG}_prof_bench
+    timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_bench -o run \
+      -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-pcie --no-census > gpurun_out/${TAG}_prof_bench.json \
+      2> gpurun_out/${TAG}_prof_bench.log
+    rc=$?; echo "[prof] exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_bench.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_bench -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_prof_bench_full.txt; head -12 gpurun_out/${TAG}_prof_bench_full.txt
+    PMC_OUT=${TAG}_pmc_bench.json bash tools/gpu_pmc_bench.sh || exit $?
+    bash tools/gpu_pmc_scatter.sh > gpurun_out/${TAG}_pmc_scatter_sq.txt 2>&1; rc=$?; tail -40 gpurun_out/${TAG}_pmc_scatter_sq.txt; exit $rc ;;
   ab)
     timeout -k 10 420 python -u bench.py --steps ${STEPS:-8} --warmup 2 --ab "$AB" --no-cpu --no-census --no-pcie \
       --flag-steps 0 ${ARGS:-} > gpurun_out/${TAG}_ab.json 2> gpurun_out/${TAG}_ab.log
