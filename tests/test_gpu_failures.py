@@ -4,7 +4,7 @@ VERDICT r4 item 1).  CRDT_TEST_FAIL="rank:point" makes one rank fail with CRDT_E
 call: 1 before the gather (staging / the scan), 2 route_l1's preparation (before its count exchange), 3 the
 receive area (before the record exchange), 4 the owners' apply (after the exchange), 5 the map-side
 combine's home fold.  Every rank must return CRDT_E_NOMEM within the test's timeout, and the same ctxs must
-then merge the whole job exactly (rows equal to the unsharded K2 merge)."""
+then merge the whole job exactly (rows equal to the C oracle's unsharded merge)."""
 import numpy as np
 import pytest
 

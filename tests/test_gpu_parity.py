@@ -571,8 +571,8 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R, calls=1):
                                                     ("0", "1", "3"), ("0", "0", "1"), ("0", "2", "1"), ("0", "2", "0"),
                                                     ("0", "2", "4")])
 def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1, split):
-    """Full-table property at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
-    routed to key % 2) give exactly the rows and canonical of the unsharded merge — with the
+    """Full-table parity at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
+    routed to key % 2) give exactly the rows and canonical of the C oracle's unsharded merge — with the
     map-side combine (each rank folds its home records per key before the exchange), with the routed
     level-1 partition (home records partitioned straight into the owners' level-1 buckets, owners from
     level 2 on; route_l1 = 2: with every owner's first level-1 digit folded at the sender, one packed maximum
@@ -583,21 +583,9 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
     monkeypatch.setenv("CRDT_ROUTE_TUNE", "0")               # the fixed rule (the tuner: the test below)
     import torch.multiprocessing as mp
 
-    from crdt_amd import DeviceTable
-    from crdt_amd.workload import gen_fanin
     from tests.test_dist_cpu import _free_port
     K, total, R = 1 << 22, 4_000_000, 128
-    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
-    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
-    t.set_merge_path("gather")                                # the reference: K2, unsharded
-    loc, own = wl["local"], wl["owned"]
-    t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
-    t.canonical = wl["c0"]
-    ref, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
-                     win_flags=False)
-    rows = t.read_rows(np.arange(K, dtype=np.uint32))
-    t.close()
-    del wl
+    ref, rows = _fanin_reference(K, total, R)                  # the C oracle, unsharded
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -625,7 +613,7 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
 def test_place_tuner_candidates_same_rows(gpu_device, monkeypatch, tries, R):
     """The level-1 placement tuner (crdt_reserve_scratch with CRDT_PLACE_TRIES candidate buffers): the
     first sorted merges run their level-1 scatter on each candidate in turn and the fastest is kept;
-    every call — on every candidate and after the choice — leaves exactly the gather path's rows.
+    every call — on every candidate and after the choice — leaves exactly the C oracle's rows.
     (2048 changesets: more than the packed key's changeset window, so a call partitions in several
     windows, every one on the candidate under trial.)"""
     from crdt_amd import DeviceTable
@@ -713,20 +701,18 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
 
 
 def _fanin_reference(K, total, R):
-    """The unsharded K2 merge of gen_fanin's whole job: (result, all rows)."""
-    from crdt_amd import DeviceTable
+    """The C oracle (oracle/merge_oracle.c, the KAT-pinned restatement) merging gen_fanin's whole job
+    unsharded: (result fields, all rows as (lt, rank, val, mod))."""
     from crdt_amd.workload import gen_fanin
+    from oracle.oracle_c import OracleTable
     wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
-    t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
-    t.set_merge_path("gather")
     loc, own = wl["local"], wl["owned"]
-    t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
-    t.canonical = wl["c0"]
-    ref, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
-                     win_flags=False)
-    rows = t.read_rows(np.arange(K, dtype=np.uint32))
-    t.close()
-    return ref, rows
+    t = OracleTable(K, 0, wl["c0"])
+    t.put_rows(*(loc[f].cpu().numpy() for f in ("slot", "lt", "rank", "val", "mod")))
+    res, _ = t.merge(*(own[f].cpu().numpy() for f in ("key", "lt", "rank", "val")), wl["owned_offsets"],
+                     wl["wall"], want_flags=False)
+    rows = tuple(np.array(t.rows[f]) for f in ("lt", "rank", "val", "mod"))
+    return res.as_dict(), rows
 
 
 def test_two_rank_route_tune(gpu_device, monkeypatch):
@@ -734,7 +720,7 @@ def test_two_rank_route_tune(gpu_device, monkeypatch):
     pieces twice, the map-side combine twice, route_l1 in four pieces, in one and in two with the head fold twice
     each, every later call the way
     whose timed call was fastest (max over the ranks, the same way on both ranks); every call leaves
-    exactly the unsharded merge's rows."""
+    exactly the C oracle's rows of the unsharded merge."""
     for k in ("CRDT_COMBINE", "CRDT_ROUTE_L1", "CRDT_ROUTE_TUNE", "CRDT_RL1_SPLIT"):
         monkeypatch.delenv(k, raising=False)
     import torch.multiprocessing as mp
