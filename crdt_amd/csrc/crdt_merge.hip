@@ -1651,10 +1651,12 @@ struct crdt_ctx {
     bool last_combined = false;
     uint32_t sparse_t = 2048;       // CRDT_SPARSE_T: packed resolve buckets of fewer records read only touched rows
     int route_l1 = 1;               // CRDT_ROUTE_L1=0: sharded order-free merges route records, owners partition;
-                                    // 2: route_l1 always with the sender-side fold of the owners' first digit
-    bool rl1_call_head = false;     // this call's route_l1 folds the owners' first level-1 digit (the Zipf head)
+                                    // 2: route_l1 always with the sender-side head fold; 3: folding every digit
+    bool rl1_call_head = false;     // this call's route_l1 folds the owners' leading level-1 digits (the Zipf head)
+    bool rl1_call_all = false;      // ... all of them (CRDT_ROUTE_L1=3: tests, A/B)
     bool last_rl1_head = false;     // ... the last routed merge's did
     uint64_t last_rl1_head_in = 0, last_rl1_head_out = 0;   // ... its head records before / after the fold
+    uint32_t last_rl1_head_digits = 0;   // ... the leading level-1 digits it folded (Dh)
     uint32_t rl1_pieces = 2;        // CRDT_RL1_SPLIT: route_l1's pipelined pieces (0 / 1: one; up to kRl1MaxPieces)
     uint32_t rl1_call_pieces = 2;   // ... this call's (the tuner's way 2 takes kRl1MaxPieces)
     uint32_t last_rl1_pieces = 0;   // ... the last routed merge's
@@ -2937,7 +2939,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_PACKED")) c->packed_resolve = atoi(e) != 0;
     if (const char* e = getenv("CRDT_FLAGS_SORTED")) c->flags_sorted = atoi(e) != 0;
     if (const char* e = getenv("CRDT_COMBINE")) c->combine = std::min(std::max(atoi(e), 0), 2);
-    if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = std::min(std::max(atoi(e), 0), 2);
+    if (const char* e = getenv("CRDT_ROUTE_L1")) c->route_l1 = std::min(std::max(atoi(e), 0), 3);
     if (const char* e = getenv("CRDT_RL1_SPLIT")) {   // 0: one piece, 1: two (the default), n: n pieces
         const int v = atoi(e);
         c->rl1_pieces = std::min<uint32_t>(v <= 0 ? 1u : v == 1 ? 2u : (uint32_t)v, kRl1MaxPieces);

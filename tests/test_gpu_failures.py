@@ -14,6 +14,7 @@ NOMEM = -3
 ROUTES = {                      # CRDT_COMBINE, CRDT_ROUTE_L1 (the routing tuner off: the fixed way)
     "route_l1": ("0", "1"),
     "route_l1_head": ("0", "2"),            # with the head fold (its own count exchange after the pieces)
+    "route_l1_all": ("0", "3"),             # ... folding every level-1 digit
     "combine": ("2", "1"),
     "records": ("0", "0"),
 }
@@ -83,7 +84,7 @@ def _run(world, K, total, R, route, point, fail_rank):
         assert st_fail == NOMEM, (rank, route, point, st_fail)           # every rank, not only the failing one
         assert st_ok == 0, (rank, st_ok)
         if route.startswith("route_l1"):
-            assert plan["route_l1"] and plan["rl1_head"] == (route == "route_l1_head"), plan
+            assert plan["route_l1"] and plan["rl1_head"] == (route != "route_l1"), plan
         if route == "combine":
             assert plan["combined"], plan
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
@@ -93,7 +94,7 @@ def _run(world, K, total, R, route, point, fail_rank):
 
 
 @pytest.mark.parametrize("route,point", [("route_l1", 1), ("route_l1", 2), ("route_l1", 3), ("route_l1", 4),
-                                         ("route_l1_head", 3), ("route_l1_head", 4),
+                                         ("route_l1_head", 3), ("route_l1_head", 4), ("route_l1_all", 4),
                                          ("combine", 1), ("combine", 5), ("combine", 3), ("combine", 4),
                                          ("records", 1), ("records", 3), ("records", 4)])
 @pytest.mark.parametrize("fail_rank", [0, 1])
@@ -102,7 +103,7 @@ def test_two_rank_injected_failure(gpu_device, route, point, fail_rank):
 
 
 @pytest.mark.parametrize("route,point", [("route_l1", 1), ("route_l1", 2), ("route_l1", 3), ("route_l1", 4),
-                                         ("route_l1_head", 3), ("route_l1_head", 4), ("records", 3)])
+                                         ("route_l1_head", 4), ("records", 3)])
 def test_eight_rank_injected_failure(gpu_device, route, point):
     """Eight ranks on one GPU (K = 2^24: shards of 2^21 slots, two level-1 digits per owner), rank 5 fails."""
     _run(8, 1 << 24, 4_000_000, 64, route, point, 5)

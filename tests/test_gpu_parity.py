@@ -569,14 +569,14 @@ def _fanin_shard_worker(rank, world, port, q, K, total, R, calls=1):
 
 @pytest.mark.parametrize("combine,route_l1,split", [("1", "1", "1"), ("0", "1", "1"), ("0", "1", "0"), ("0", "1", "4"),
                                                     ("0", "1", "3"), ("0", "0", "1"), ("0", "2", "1"), ("0", "2", "0"),
-                                                    ("0", "2", "4")])
+                                                    ("0", "2", "4"), ("0", "3", "1")])
 def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, route_l1, split):
     """Full-table parity at a fan-in shape: 2 ranks (replica j whole on rank j % 2, records
     routed to key % 2) give exactly the rows and canonical of the C oracle's unsharded merge — with the
     map-side combine (each rank folds its home records per key before the exchange), with the routed
     level-1 partition (home records partitioned straight into the owners' level-1 buckets, owners from
-    level 2 on; route_l1 = 2: with every owner's first level-1 digit folded at the sender, one packed maximum
-    per key, sent after the pieces), and with plain record routing."""
+    level 2 on; route_l1 = 2: with every owner's leading level-1 digits folded at the sender, one packed
+    maximum per key, sent after the pieces; 3: every digit folded), and with plain record routing."""
     monkeypatch.setenv("CRDT_COMBINE", combine)
     monkeypatch.setenv("CRDT_ROUTE_L1", route_l1)
     monkeypatch.setenv("CRDT_RL1_SPLIT", split)             # route_l1 in two pipelined pieces / in one
@@ -600,7 +600,7 @@ def test_two_rank_routed_fanin_equals_one_gpu(gpu_device, monkeypatch, combine, 
         assert path == "sorted"
         assert plan["combined"] == (combine == "1"), plan
         assert plan["route_l1"] == (combine == "0" and route_l1 != "0"), plan
-        assert plan["rl1_head"] == (plan["route_l1"] and route_l1 == "2"), plan
+        assert plan["rl1_head"] == (plan["route_l1"] and route_l1 in ("2", "3")), plan
         if plan["route_l1"]:                                   # pieces cut at changeset boundaries
             assert plan["rl1_pieces"] == {"0": 1, "1": 2}.get(split, int(split)), plan
         for f in ("status", "n_stored", "canonical_lt", "exc_changeset"):
@@ -672,7 +672,7 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
     t.comm_init_ops(G, 0, comm)
     ways = {"1": ("0", "1", "0", 1), "2": ("0", "1", "1", 2), "3": ("0", "1", "3", 3), "4": ("0", "1", "4", 4),
             "route": ("0", "0", "1", 0), "fold": ("2", "1", "1", 0), "head": ("0", "2", "1", 2),
-            "head1": ("0", "2", "0", 1)}
+            "head1": ("0", "2", "0", 1), "headall": ("0", "3", "1", 2)}
     rows = {}
     for name, (comb, rl1, split, pieces) in ways.items():
         monkeypatch.setenv("CRDT_COMBINE", comb)
@@ -790,15 +790,14 @@ def test_eight_rank_routed_packed_sorted(gpu_device, monkeypatch, inject, combin
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res
 
 
-@pytest.mark.parametrize("head", ["1", "2"])
-@pytest.mark.parametrize("inject", [None, "drift", "dup"])
+@pytest.mark.parametrize("inject,head", [(None, "1"), ("drift", "1"), ("dup", "1"), ("dup", "2"), ("drift", "3")])
 def test_eight_rank_route_l1(gpu_device, monkeypatch, inject, head):
     """The routed level-1 partition at G = 8 (comm_path.inc, route_l1): shards of > 2^20 slots (two
     digits per owner), 16M records in 64 changesets, every rank partitioning its home records straight
     into the 8 owners' level-1 buckets (14-B records over the exchange, own part in place), the owners
     from level 2 on; a drift or duplicate-node record at (41, 123,456).  Every row of all 8 shards,
     canonical, status and exception fields vs the C oracle, on two calls per ctx (buffers reused).
-    head = 2: every owner's first level-1 digit folded at the sender (CRDT_ROUTE_L1=2)."""
+    head = 2: every owner's leading level-1 digits folded at the sender (CRDT_ROUTE_L1=2); 3: every digit."""
     monkeypatch.setenv("CRDT_ROUTE_L1", head)
     kw = dict(seed=818, R=64, per_cs=250_000, n_local=6_000_000, n_new=3_000_000, millis_span=1 << 12,
               counter_span=16, n_ranks=65, tomb_frac=0.1, inject=inject)
@@ -806,7 +805,7 @@ def test_eight_rank_route_l1(gpu_device, monkeypatch, inject, head):
     for rank, res, *_ in outs:
         assert res["path"] == "sorted" and res["plan"]["route_l1"], (rank, res["plan"])
         assert not res["plan"]["combined"], (rank, res["plan"])
-        assert res["plan"]["rl1_head"] == (head == "2"), (rank, res["plan"])
+        assert res["plan"]["rl1_head"] == (head != "1"), (rank, res["plan"])
         assert res["status"] == {None: 0, "drift": 1, "dup": 2}[inject], res
         if inject:
             assert (res["exc_changeset"], res["exc_index"]) == (41, 123_456), res

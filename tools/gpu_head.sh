@@ -10,6 +10,8 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
     > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
   tail -3 gpurun_out/${TAG}_tests.log
 fi
-N=${N:-8} STEPS=${STEPS:-2} MODES=${MODES:-route_l1,route_l1_head} timeout -k 10 600 python -u tools/route_probe.py \
-  > gpurun_out/${TAG}_probe.log 2>&1 || { tail -30 gpurun_out/${TAG}_probe.log; exit 1; }
-grep -E "mean|rows" gpurun_out/${TAG}_probe.log
+for n in ${NS:-8}; do
+  N=$n STEPS=${STEPS:-2} MODES=${MODES:-route_l1,route_l1_head} timeout -k 10 600 python -u tools/route_probe.py \
+    > gpurun_out/${TAG}_probe_n$n.log 2>&1 || { tail -30 gpurun_out/${TAG}_probe_n$n.log; exit 1; }
+  echo "N=$n"; grep -E "mean|rows" gpurun_out/${TAG}_probe_n$n.log
+done

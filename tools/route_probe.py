@@ -35,7 +35,8 @@ ENV = {"route_l1": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT":
        "route_l1_4piece": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "1", "CRDT_RL1_SPLIT": "4"},
        "route": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "0"},
        "combine": {"CRDT_COMBINE": "2", "CRDT_ROUTE_L1": "1"},
-       "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2", "CRDT_RL1_SPLIT": "1"}}
+       "route_l1_head": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "2", "CRDT_RL1_SPLIT": "1"},
+       "route_l1_all": {"CRDT_COMBINE": "0", "CRDT_ROUTE_L1": "3", "CRDT_RL1_SPLIT": "1"}}
 
 wl = gen_fanin(total=1_000_000_512, R=1024, K=1 << 28, n_local=1 << 27, s=0.8, device="cuda", rank=0, world=N,
                route=True)
