@@ -2544,8 +2544,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             tm2f = tm2;
             nt2f = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            if (k16 && !(c->form_off & kFormNoHistW))   // key bits [4, 20) in 2 B: the level-2 digit
-                k_part_hist16w<<<nt2, kHThreads, 0, c->stream>>>(         // (bits [12, 20)) is its high byte
+            if (k16 && !(c->form_off & kFormNoHistW) && ts2 == (uint32_t)kPTile2)   // key bits [4, 20) in 2 B:
+                k_part_hist16w<256, kPTile2><<<nt2, 256, 0, c->stream>>>(   // the level-2 digit (bits [12, 20))
+                    reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, h2p);   // is its high byte
+            else if (k16 && !(c->form_off & kFormNoHistW))
+                k_part_hist16w<<<nt2, kHThreads, 0, c->stream>>>(
                     reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, h2p);
             else if (k16)
                 k_part_hist<false, true><<<nt2, kHThreads, 0, c->stream>>>(p1k, tm2, 0, c->d_misc, c->cap,
