@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 TIMING_EVERY = 8           # streaming configs (one merge call per delta): HIP-event timing sampled
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_bench.json")    # rocprofv3 --pmc of the default command
+PMC_FILE = os.path.join(ROOT, "profiles", "r05b_pmc_bench.json")    # rocprofv3 --pmc of the default command
 
 
 def log(*a):
@@ -333,7 +333,7 @@ def main():
             tm = {k: sum(t[k] for t in tms) for k in tms[0]}
             if wl.get("per_call"):                   # sampled calls -> per-step estimates
                 f = wl["R"] / len(tms)
-                for k in ("scan_ms", "clock_ms", "route_ms", "total_ms"):
+                for k in ("scan_ms", "clock_ms", "route_ms", "total_ms", "sent_bytes"):
                     tm[k] *= f
                 tm["apply_total"] = int(round(tm["apply_total"] * f))
             for k, v in tm.items():
@@ -680,6 +680,11 @@ def main():
                          "device_total": round(tsum.get("total_ms", 0) / K, 3)},
     }
     beat.stop()
+    if world > 1:
+        # the bytes this rank handed its peers per timed step (crdt_timing.sent_bytes), max over the ranks
+        out["exchange"] = {"bytes_per_rank_per_step": int(all_max(tsum.get("sent_bytes", 0) / K)),
+                           "plan": {k: v for k, v in table.last_plan().items()
+                                    if k in ("route_l1", "rl1_head", "combined", "rl1_pieces")}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     table.close()

@@ -50,7 +50,8 @@ class CrdtTiming(ctypes.Structure):
                 ("apply_ms", ctypes.c_double), ("apply_launches", ctypes.c_uint32),
                 ("apply_total", ctypes.c_uint32), ("total_ms", ctypes.c_double),
                 ("route_ms", ctypes.c_double), ("part1_ms", ctypes.c_double), ("part2_ms", ctypes.c_double),
-                ("resolve_ms", ctypes.c_double), ("part1_records", ctypes.c_uint64)]
+                ("resolve_ms", ctypes.c_double), ("part1_records", ctypes.c_uint64),
+                ("sent_bytes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

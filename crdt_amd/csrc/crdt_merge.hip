@@ -1657,6 +1657,7 @@ struct crdt_ctx {
     bool last_rl1_head = false;     // ... the last routed merge's did
     uint64_t last_rl1_head_in = 0, last_rl1_head_out = 0;   // ... its head records before / after the fold
     uint32_t last_rl1_head_digits = 0;   // ... the leading level-1 digits it folded (Dh)
+    uint64_t sent_bytes = 0;        // this call's bytes to the peers (comm_all_to_all; crdt_timing.sent_bytes)
     uint32_t rl1_pieces = 2;        // CRDT_RL1_SPLIT: route_l1's pipelined pieces (0 / 1: one; up to kRl1MaxPieces)
     uint32_t rl1_call_pieces = 2;   // ... this call's (the tuner's way 2 takes kRl1MaxPieces)
     uint32_t last_rl1_pieces = 0;   // ... the last routed merge's
@@ -2898,6 +2899,7 @@ void collect_timing(crdt_ctx* c) {
             t.part1_records = c->p1_records;
         }
     }
+    t.sent_bytes = c->sent_bytes;
     c->last_timing = t;
 }
 
@@ -3330,6 +3332,7 @@ int crdt_merge(crdt_ctx* c, const crdt_batch* batch, int64_t wall, uint8_t* win_
         crdt_ctx* c;
         ~HwUpdate() { c->hw = std::max(c->hw, c->hw_next); }
     } hw_update{c};
+    c->sent_bytes = 0;
     if (c->has_comm) return merge_sharded(c, batch, wall, win_flags, out);
     c->place_timed = c->place_warm = false;                  // (set by this call's first sorted window)
     // Host batches are staged once; every phase then sees device columns.

@@ -39,7 +39,7 @@ extern "C" {
 #endif
 
 #define CRDT_ABI_VERSION 4          /* 3: crdt_timing gained part1_records (round 3); 4: crdt_route_tune_info
-                                       reports five ways (round 5) */
+                                       reports five ways, crdt_timing gained sent_bytes (round 5) */
 #define CRDT_NULL_VALUE 0xFFFFFFFFu
 
 /* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
@@ -114,6 +114,9 @@ typedef struct crdt_timing {
     double part2_ms;
     double resolve_ms;
     uint64_t part1_records;    /* records the level-1 partition scatter read in that window */
+    uint64_t sent_bytes;       /* sharded ctx: bytes this rank handed its peers in the call's all-to-all
+                                  exchanges (records, counts; its own part excluded); 0 on one GPU.
+                                  Filled whether or not timing is on. */
 } crdt_timing;
 
 /* ---- lifecycle ------------------------------------------------------------ */

@@ -685,6 +685,8 @@ def test_loopback_route_ways_same_rows(gpu_device, monkeypatch, G):
             res, _ = t.merge(home["key"], home["lt"], home["rank"], home["val"], wl["home_offsets"], wl["wall"],
                              win_flags=False)
             assert res["status"] == 0 and comm.error is None, (name, res, comm.error)
+            # crdt_timing.sent_bytes: what the library handed the communicator for its peers
+            assert t.timing()["sent_bytes"] == comm.exchange_bytes() > 0, name
             plan = t.last_plan()
             assert plan["route_l1"] == (pieces > 0) and plan["rl1_pieces"] == pieces, (name, plan)
             assert plan["combined"] == (name == "fold"), (name, plan)

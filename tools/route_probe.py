@@ -68,7 +68,7 @@ for it in range(STEPS + 1):
         tm = t.timing()
         plan = t.last_plan()
         line = (f"{m:9s} step {it}: wall {wall_ms:.2f} ms, device {tm['total_ms']:.2f}, exchange copy {xms:.2f} "
-                f"({xgb:.3f} GB sent), "
+                f"({xgb:.3f} GB sent; library {tm['sent_bytes'] / 1e9:.3f}), "
                 f"local {tm['total_ms'] - xms:.2f} | scan {tm['scan_ms']:.2f} clock {tm['clock_ms']:.2f} "
                 f"route {tm['route_ms']:.2f} L1 {tm['part1_ms']:.2f} L2 {tm['part2_ms']:.2f} "
                 f"resolve {tm['resolve_ms']:.2f} | route_l1 {plan['route_l1']} head {plan['rl1_head']} "
