@@ -2694,8 +2694,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw + 8));
 #define CRDT_FBACK2(CHK)                                                                                  \
-    k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,           \
-                                                          c->f_flag1.p, c->d_misc)
+    if (tm2f.tsize == (uint32_t)kPTile2)                                                                  \
+        k_flags_back<false, CHK, kPTile2><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p,       \
+                                                                       c->f_flag2.p, c->f_flag1.p, c->d_misc); \
+    else                                                                                                  \
+        k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,       \
+                                                              c->f_flag1.p, c->d_misc)
                 if (c->fback_chk == 4) { CRDT_FBACK2(4); }
                 else if (c->fback_chk == 6) { CRDT_FBACK2(6); }
                 else { CRDT_FBACK2(0); }

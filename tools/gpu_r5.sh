@@ -59,7 +59,7 @@ if [ "${STAGE}" = "libab" ]; then
       if [ "$lib" = new ]; then unset CRDT_LIB_PATH; else export CRDT_LIB_PATH=$lib; fi
       timeout -k 10 300 python -u bench.py --steps ${STEPS:-6} --warmup 2 --no-cpu --no-census --no-pcie --flag-steps 0 ${ARGS:-} \
         > gpurun_out/${TAG}_libab_${i}_$(basename $lib).json 2> gpurun_out/${TAG}_libab_${i}_$(basename $lib).log || exit $?
-      python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_libab_${i}_$(basename $lib).json')); ph=d['roofline']['dominant_kernel']['phases_ms_per_step']; print('$lib', d['ms_per_step'], ph, (d.get('placement') or {}).get('level1_ms'))"
+      python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_libab_${i}_$(basename $lib).json')); ph=d['roofline']['dominant_kernel']['phases_ms_per_step']; print('$lib', d['ms_per_step'], ph, (d.get('placement') or {}).get('level1_ms'), 'flags', (d.get('with_win_flags') or {}).get('ms_per_step'))"
     done
   done
 fi
