@@ -683,7 +683,7 @@ def main():
     if world > 1:
         # the bytes this rank handed its peers per timed step (crdt_timing.sent_bytes), max over the ranks
         out["exchange"] = {"bytes_per_rank_per_step": int(all_max(tsum.get("sent_bytes", 0) / K)),
-                           "plan": {k: v for k, v in table.last_plan().items()
+                           "plan": {k: v for k, v in plan.items()          # (the timed steps' way)
                                     if k in ("route_l1", "rl1_head", "combined", "rl1_pieces")}}
     if rank == 0:
         print(json.dumps(out), flush=True)
