@@ -129,6 +129,50 @@ class Heartbeat:
         self._stop.set()
 
 
+class Watchdog:
+    """Every rank's bound on one collective merge call (N > 1).  The library ends a call
+    whose peer is lost at its own deadline (crdt_set_comm_timeout: CRDT_E_COMM); this catches what it cannot
+    see — a rank stuck outside a collective merge, or inside RCCL's host calls (connection setup).  When a
+    call overruns it prints this rank's phase, the library's phase and last plan, and exits the process
+    non-zero (os._exit: no exec), so the launcher ends the job with a diagnosis instead of a timeout."""
+
+    def __init__(self, rank: int):
+        import threading
+        self.rank = rank
+        self.table = None
+        self.what = None
+        self.deadline = None
+        self._lock = threading.Lock()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def arm(self, seconds: float, what: str):
+        with self._lock:
+            self.what, self.deadline = what, time.monotonic() + seconds
+
+    def disarm(self):
+        with self._lock:
+            self.deadline = None
+
+    def _run(self):
+        while True:
+            time.sleep(0.5)
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                what = self.what
+            if not late:
+                continue
+            lib = plan = None
+            try:
+                lib = self.table.comm_state() if self.table is not None else None
+                plan = self.table.last_plan() if self.table is not None else None
+            except Exception as e:  # noqa: BLE001 -- the report must go out whatever the table's state
+                lib = f"unreadable: {e!r}"
+            print(f"[bench] rank {self.rank}: WATCHDOG: {what} overran its bound; library (state, phase) {lib}; "
+                  f"last plan {plan}", file=sys.stderr, flush=True)
+            os._exit(4)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -162,6 +206,12 @@ def parse():
                         "(cfg2, cfg5: random winner writes), else 24")
     p.add_argument("--late-alloc", action="store_true",
                    help="create the table after the workload (the library allocates its scratch in the first merge)")
+    p.add_argument("--comm-timeout", type=float, default=120.0,
+                   help="N > 1: one collective merge's deadline in s inside the library (crdt_set_comm_timeout)")
+    p.add_argument("--call-timeout", type=float, default=300.0,
+                   help="N > 1: every rank's watchdog bound on one merge call in s (then it reports and exits)")
+    p.add_argument("--dist-timeout", type=float, default=1800.0,
+                   help="N > 1: torch.distributed's timeout in s (barriers, the parity gather)")
     p.add_argument("--ab", default=None, metavar="VAR=v1,v2",
                    help="development A/B: the timed steps alternate the library switch VAR over the values "
                         "(one process, one memory placement); per-value step times go to stderr")
@@ -188,11 +238,15 @@ def main():
     # CRDT_BENCH_BACKEND=gloo: rehearsal of N ranks on one GPU (RCCL needs one GPU per rank); the
     # library then exchanges through dist.GlooComm (host-staged) instead of its RCCL communicator
     backend = os.environ.get("CRDT_BENCH_BACKEND", "nccl")
+    watchdog = None
     if world > 1:
+        import datetime
+        to = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=to)
+        watchdog = Watchdog(rank)
     from crdt_amd import DeviceTable
     from crdt_amd.dist import GlooComm, attach_rccl
     from crdt_amd.workload import gen_cfg2, gen_cfg3, gen_cfg5, gen_fanin
@@ -257,6 +311,10 @@ def main():
             attach_rccl(table, dist)                 # RCCL communicator inside the ctx
         else:
             table.comm_init_ops(world, rank, GlooComm(dist))
+        # a lost peer ends a call at this deadline (CRDT_E_COMM) on every surviving rank; the watchdog bounds
+        # the whole call on each rank
+        table.set_comm_timeout(int(args.comm_timeout * 1e3))
+        watchdog.table = table
     loc = wl["local"]
     src = wl["home"] if world > 1 else wl["owned"]
     offs = wl["home_offsets"] if world > 1 else wl["owned_offsets"]
@@ -270,12 +328,23 @@ def main():
         torch.cuda.synchronize()
 
     def step(flags=None):
+        if watchdog is not None:
+            watchdog.arm(args.call_timeout, f"merge step ({beat.phase})")
+        try:
+            return step_(flags)
+        finally:
+            if watchdog is not None:
+                watchdog.disarm()
+
+    def step_(flags=None):
         if wl.get("per_call"):                       # streaming: one crdt_merge per delta
             tot = None
             for d in range(wl["R"]):
                 b, e = int(offs[d]), int(offs[d + 1])
                 fl = False if flags is None else flags[b:e]
                 sample = table_timing[0] and d % TIMING_EVERY == 0      # HIP events on every 8th call only
+                if watchdog is not None:
+                    watchdog.arm(args.call_timeout, f"merge of delta {d} ({beat.phase})")
                 if table_timing[0]:
                     table.set_timing(sample)
                 r, _ = table.merge(*delta_cols[d], int(wl["walls"][d]), win_flags=fl)

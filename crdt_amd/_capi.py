@@ -75,7 +75,7 @@ class CrdtCommOps(ctypes.Structure):
 
 
 COMM_ID_BYTES = 128
-ABI_VERSION = 4                            # include/crdt_merge.h CRDT_ABI_VERSION
+ABI_VERSION = 5                            # include/crdt_merge.h CRDT_ABI_VERSION
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -110,6 +110,8 @@ SIGNATURES = {
     "crdt_comm_info": (_INT, [_P, _P, _P]),
     "crdt_comm_free": (_INT, [_P]),
     "crdt_set_presharded": (_INT, [_P, _INT]),
+    "crdt_set_comm_timeout": (_INT, [_P, _U32]),
+    "crdt_comm_state": (_INT, [_P, _P, _P]),
     "crdt_set_merge_path": (_INT, [_P, _INT]),
     "crdt_set_counts": (_INT, [_P, _INT]),
     "crdt_set_rank_bound": (_INT, [_P, _U32]),

@@ -26,8 +26,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -1528,6 +1532,9 @@ constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histo
 constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
 constexpr uint32_t kFormNoOwnInPlace = 524288; // sharded merge: the own chunk copied to the receive columns
+constexpr uint32_t kFormNoFbackXcd = 1u << 21;   // flag passes: plain tile order (not the scatters' XCD order)
+constexpr uint32_t kFormNoFbackWide = 1u << 22;  // flag passes: one staged byte per load (CRDT_FBACK_CHK applies)
+constexpr uint32_t kFormNoOverlap = 1u << 23;    // sorted path: split buckets' fold / carry not beside the resolve
 constexpr uint32_t kPartPad = 1024;          // records of slack behind every partition buffer (tile-end vector loads)
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
@@ -1687,6 +1694,7 @@ struct crdt_ctx {
     DBuf<unsigned long long> rl_hcnt;   // ... [G] sent, [G] received, [1] own, [G] bases
     HBuf<unsigned long long> h_hcnt;
     hipEvent_t rl_evh = nullptr;    // ... the fold is done (side stream)
+    hipEvent_t ov_ev[2] = {};       // sorted path: the split buckets' fold forks to sstream / joins back
     DBuf<uint32_t> e_key, e_val;    // the combine's emitted (key, packed key, value) list
     DBuf<uint64_t> e_pk;
     DBuf<unsigned long long> e_cnt, e_cur;
@@ -1737,6 +1745,16 @@ struct crdt_ctx {
     bool finish_posted = false;                           // this call's finish_apply posted its reduction
     // CRDT_TEST_FAIL="rank:point" (tests): this rank fails with CRDT_E_NOMEM at that point of a sharded merge
     int fail_rank = -1, fail_at = 0;
+    // the call's deadline (crdt_set_comm_timeout; comm_path.inc, "the call's deadline"): every host wait of a
+    // sharded call polls against it; past it the communicator is aborted and the call returns CRDT_E_COMM
+    uint32_t comm_timeout_ms = 300000;
+    int64_t comm_deadline_ns = 0;                         // this call's (steady clock; 0: none)
+    std::atomic<int> comm_state{0};                       // 0 usable, 1 aborted (deadline), 2 aborted (transport)
+    std::atomic<const char*> comm_phase{"idle"};          // where the current / last sharded call is (static text)
+    // CRDT_TEST_STALL="rank:point:ms[:d]" (tests): that rank stalls ms at that point (host sleep, or with :d a
+    // bounded device spin on the ctx stream); ms < 0: the process exits there (a peer lost mid-call)
+    int stall_rank = -1, stall_at = 0, stall_ms = 0;
+    bool stall_dev = false;
 };
 
 // The level-1 partition tile (records).  The default and 14336 / 28672 are tiles the scan's fused histogram
@@ -1768,6 +1786,23 @@ namespace {
         if (_e != hipSuccess) return CRDT_E_HIP;                           \
     } while (0)
 
+// A HIP failure between two collectives of a sharded call: kept in the call's local status `lst` (the rank
+// still posts the collectives, carrying it) instead of returning at once (comm_path.inc, "failures agreed").
+#define HIPLST(expr)                                                       \
+    do {                                                                   \
+        hipError_t _e = (expr);                                            \
+        if (_e != hipSuccess && !lst) lst = CRDT_E_HIP;                    \
+    } while (0)
+
+// A host wait for the ctx's stream (or an event).  On a sharded ctx joined to a device transport it polls
+// against the call's deadline and the transport's asynchronous error (comm_path.inc, comm_wait).
+int comm_wait(crdt_ctx* c, hipStream_t s, hipEvent_t e = nullptr);
+#define SYNCHK(c, s)                                                       \
+    do {                                                                   \
+        int _w = comm_wait((c), (s));                                      \
+        if (_w) return _w;                                                 \
+    } while (0)
+
 inline unsigned grid_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
 hipError_t ensure_events(crdt_ctx* c, size_t n) {
@@ -1778,6 +1813,22 @@ hipError_t ensure_events(crdt_ctx* c, size_t n) {
         c->events.push_back(e);
     }
     return hipSuccess;
+}
+
+// The sorted path's two-stream resolve: sstream starts behind everything queued on the ctx stream (fork); the
+// ctx stream continues behind everything queued on sstream (join).
+int overlap_fork(crdt_ctx* c) {
+    if (!c->sstream) HIPCHK(hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->ov_ev)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ov_ev[0], c->stream));
+    HIPCHK(hipStreamWaitEvent(c->sstream, c->ov_ev[0], 0));
+    return CRDT_OK;
+}
+int overlap_join(crdt_ctx* c) {
+    HIPCHK(hipEventRecord(c->ov_ev[1], c->sstream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ov_ev[1], 0));
+    return CRDT_OK;
 }
 
 // Stage a host-memory column into ctx device memory; device-memory columns pass through.
@@ -2079,6 +2130,7 @@ int kv_copy_all(crdt_ctx* c) {
 }
 
 int comm_all_reduce(crdt_ctx* c, long long* d, uint64_t n, int32_t op);   // comm_path.inc
+void test_stall(crdt_ctx* c, int point);                                   // ... (CRDT_TEST_STALL)
 
 // The sorted path's frame from the scan's accumulators (read back into h_misc); with a declared
 // rank bound its rank part is [0, bound) — the level-1 scatter checks every rank against it.
@@ -2107,6 +2159,7 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
         k_sum_counts<<<1, 64, 0, c->stream>>>(c->d_misc, counted, c->d_sum.p, local_st);
         int st = comm_all_reduce(c, c->d_sum.p, kSumWords + kSumCodes, CRDT_REDUCE_SUM);
         if (st) return st;
+        test_stall(c, 5);                   // (kStallReadback: a device spin behind the reduction, tests)
         HIPCHK(hipMemcpyAsync(c->h_sum.p, c->d_sum.p, (kSumWords + kSumCodes) * sizeof(long long),
                               hipMemcpyDeviceToHost, c->stream));
     } else if (local_st) {
@@ -2114,7 +2167,7 @@ int finish_apply(crdt_ctx* c, uint8_t* host_flags, const uint8_t* dflags, uint64
     }
     HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
     if (host_flags && n && !local_st) HIPCHK(hipMemcpyAsync(host_flags, dflags, n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    SYNCHK(c, c->stream);
     if (c->has_comm)                        // a rank's failure (the largest code) is every rank's
         for (int k = kSumCodes - 1; k > 0; --k)
             if (c->h_sum.p[kSumWords + k]) return -k;
@@ -2336,7 +2389,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     bool pk = false;
     if (cols.packed_in || (c->packed_resolve && c->frame_on)) {
         HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        SYNCHK(c, c->stream);
         pf = frame_of(c);
         pk = pf.ok;
         if (cols.packed_in && !pk) return CRDT_E_INVALID;           // routed packed under this same frame
@@ -2374,7 +2427,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (nw == 0) continue;
         // host plan: segment bounds and changesets, level-1 tile prefix, the one-segment scan map
         // (the pinned staging buffer is reused: the previous window's copy must have run)
-        if (s0 > 0) HIPCHK(hipStreamSynchronize(c->stream));
+        if (s0 > 0) SYNCHK(c, c->stream);
         const size_t u32_words = (2 * (size_t)nseg + 2) / 2;        // seg_j [nseg] + tb [nseg + 1]
         const size_t words = 2 * (size_t)nseg + u32_words + 3;
         HIPALLOC(c->h_pplan.ensure(words));
@@ -2615,6 +2668,8 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         KeyState ps{c->p_kslt.p, c->p_ksu32.p, c->p_ksu32.p + ksn, c->p_ksu32.p + 2 * ksn};
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
+        // split buckets (parts folded apart, then carried) beside the unsplit buckets' resolve: two streams
+        const bool ov = !em && pk && (ord || !c->counts) && two && !(c->form_off & kFormNoOverlap);
         if (ph) ev_record(c, ev_window(3, false));
         if (em) HIPALLOC(c->e_bbase.ensure(nb));
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc,
@@ -2669,53 +2724,67 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             HIPALLOC(c->f_cin_pres.ensure(ksn));
             if (fl) HIPALLOC(c->f_flag2.ensure(nw + 8));
             uint8_t* fl2 = fl ? c->f_flag2.p : nullptr;
+            // the split buckets' part folds and carry-ins on the side stream, beside the unsplit buckets' ordered
+            // resolve (disjoint buckets: their rows, states and flags do not meet); then the split buckets' walk
+            int st = ov ? overlap_fork(c) : CRDT_OK;
+            if (st) return st;
+            const hipStream_t fs = ov ? c->sstream : c->stream;
             if (k8)
-                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
                     ps_val, pf, c->d_misc);
             else
-                k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
                     ps_val, pf, c->d_misc);
-            k_part_cin_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+            k_part_cin_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, fs>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
                 reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
-            if (k8)
-                k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
-                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);
-            else
-                k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, cink,
-                    c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2);
+            for (uint32_t which = ov ? 1u : 0u; which <= (ov ? 2u : 0u); ++which) {
+                if (which == 2 && (st = overlap_join(c))) return st;
+                if (k8)
+                    k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                        cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
+                else
+                    k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                        cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
+            }
             // flags back: level-2 order -> level-1 order (two levels) -> input order
             const uint8_t* f1 = c->f_flag2.p;
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw + 8));
-#define CRDT_FBACK2(CHK)                                                                                  \
+                const bool fx = c->xcd_map && !(c->form_off & kFormNoFbackXcd);
+                const uint32_t xf2 = fx ? (nt2f + kXcds - 1) / kXcds : 0;
+#define CRDT_FBACK2(CHK, W)                                                                               \
     if (tm2f.tsize == (uint32_t)kPTile2)                                                                  \
-        k_flags_back<false, CHK, kPTile2><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p,       \
-                                                                       c->f_flag2.p, c->f_flag1.p, c->d_misc); \
+        k_flags_back<false, CHK, kPTile2, W><<<xcd_grid(nt2f, fx), 512, 0, c->stream>>>(                  \
+            tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc, xf2);                     \
     else                                                                                                  \
-        k_flags_back<false, CHK><<<nt2f, 512, 0, c->stream>>>(tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p,       \
-                                                              c->f_flag1.p, c->d_misc)
-                if (c->fback_chk == 4) { CRDT_FBACK2(4); }
-                else if (c->fback_chk == 6) { CRDT_FBACK2(6); }
-                else { CRDT_FBACK2(0); }
+        k_flags_back<false, CHK, kPTile, W><<<xcd_grid(nt2f, fx), 512, 0, c->stream>>>(                   \
+            tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc, xf2)
+                if (!(c->form_off & kFormNoFbackWide)) { CRDT_FBACK2(6, true); }
+                else if (c->fback_chk == 4) { CRDT_FBACK2(4, false); }
+                else if (c->fback_chk == 6) { CRDT_FBACK2(6, false); }
+                else { CRDT_FBACK2(0, false); }
 #undef CRDT_FBACK2
                 f1 = c->f_flag1.p;
                 // level 2 reused the tile -> segment index: rebuild level 1's
                 k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
                                                                                                  c->p_tseg.p);
             }
-#define CRDT_FBACK1(CHK)                                                                                  \
-    k_flags_back<true, CHK><<<nt1, 512, 0, c->stream>>>(tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags,       \
-                                                        c->d_misc)
+            const bool fx1 = c->xcd_map && !(c->form_off & kFormNoFbackXcd);
+            const uint32_t xf1 = fx1 ? (nt1 + kXcds - 1) / kXcds : 0;
+#define CRDT_FBACK1(CHK, W)                                                                               \
+    k_flags_back<true, CHK, kPTile, W><<<xcd_grid(nt1, fx1), 512, 0, c->stream>>>(                        \
+        tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc, xf1)
             if (fl) {
-                if (c->fback_chk == 4) { CRDT_FBACK1(4); }
-                else if (c->fback_chk == 6) { CRDT_FBACK1(6); }
-                else { CRDT_FBACK1(0); }
+                if (!(c->form_off & kFormNoFbackWide)) { CRDT_FBACK1(6, true); }
+                else if (c->fback_chk == 4) { CRDT_FBACK1(4, false); }
+                else if (c->fback_chk == 6) { CRDT_FBACK1(6, false); }
+                else { CRDT_FBACK1(0, false); }
             }
 #undef CRDT_FBACK1
         } else if (c->counts) {
@@ -2729,15 +2798,20 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             uint64_t* ps_key = reinterpret_cast<uint64_t*>(c->p_kslt.p);
             uint32_t* ps_val = c->p_ksu32.p;
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
+            // the split buckets' part folds + carry (they write the split buckets' rows) on the side stream, beside
+            // the unsplit buckets' resolve (the other rows): disjoint buckets, joined before the next window
+            int st = ov ? overlap_fork(c) : CRDT_OK;
+            if (st) return st;
+            const hipStream_t fs = ov ? c->sstream : c->stream;
             if (k8)
-                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             else
-                k_resolve_packed<true><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
-            k_part_carry_packed<false><<<dim3(kSKeys / 256, max_hot), 256, 0, c->stream>>>(
+            k_part_carry_packed<false><<<dim3(kSKeys / 256, max_hot), 256, 0, fs>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
             if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
                 k_resolve_packed<false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
@@ -2755,6 +2829,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc, EmitOut{}, c->sparse_t);
+            if (ov && (st = overlap_join(c))) return st;
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
                                                                           rv, c->table, c->cap, c->d_Rj.p, jb, ps, cy,
@@ -2826,7 +2901,7 @@ int apply_segs(crdt_ctx* c, const Cols& cols, uint64_t n, int32_t mem, int64_t w
         bool ok = mem == CRDT_MEM_DEVICE && c->frame_on && !cols.packed_in;
         if (ok) {
             HIPCHK(hipMemcpyAsync(c->h_misc, c->d_misc, sizeof(Misc), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
+            SYNCHK(c, c->stream);
             ok = frame_of(c).ok;
         }
         c->last_sorted = ok;
@@ -2970,6 +3045,15 @@ static void read_env_knobs(crdt_ctx* c) {
         int r = -1, at = 0;
         if (sscanf(e, "%d:%d", &r, &at) == 2) { c->fail_rank = r; c->fail_at = at; }
     }
+    c->stall_rank = -1;
+    c->stall_at = c->stall_ms = 0;
+    c->stall_dev = false;
+    if (const char* e = getenv("CRDT_TEST_STALL")) {    // "rank:point:ms[:d]" (comm_path.inc, test_stall)
+        int r = -1, at = 0, ms = 0;
+        char d = 0;
+        const int k = sscanf(e, "%d:%d:%d:%c", &r, &at, &ms, &d);
+        if (k >= 3) { c->stall_rank = r; c->stall_at = at; c->stall_ms = ms; c->stall_dev = k == 4 && d == 'd'; }
+    }
 }
 
 int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** out) {
@@ -2990,6 +3074,7 @@ int crdt_create(int device, uint32_t local_rank, uint64_t capacity, crdt_ctx** o
     }
     read_env_knobs(c);
     if (const char* e = getenv("CRDT_ENV_DYNAMIC")) c->env_dynamic = atoi(e) != 0;
+    if (const char* e = getenv("CRDT_COMM_TIMEOUT_MS")) c->comm_timeout_ms = (uint32_t)std::max(atoll(e), 0ll);
     if (const char* e = getenv("CRDT_KV_WINDOW")) {
         const long long v = atoll(e);
         if (v > 0) c->kv_window = (uint64_t)v;
@@ -3023,6 +3108,7 @@ void crdt_destroy(crdt_ctx* c) {
     for (hipEvent_t e : c->rl_evx) if (e) hipEventDestroy(e);
     if (c->rl_evo) hipEventDestroy(c->rl_evo);
     if (c->rl_evh) hipEventDestroy(c->rl_evh);
+    for (hipEvent_t e : c->ov_ev) if (e) hipEventDestroy(e);
     if (c->sstream) hipStreamDestroy(c->sstream);
     if (c->ostream) hipStreamDestroy(c->ostream);
     if (c->table.base) hipFree(c->table.base);

@@ -265,6 +265,25 @@ class DeviceTable:
         ops = comm.ops()
         st = self._lib.crdt_comm_init_ops(self._ctx, n_ranks, rank, ctypes.byref(ops))
         self._check(st, "crdt_comm_init_ops")
+        ms = getattr(self, "_comm_timeout_ms", None)       # (a deadline set before: the transport's bound too)
+        if ms is not None and hasattr(comm, "timeout") and comm.timeout is None:
+            comm.timeout = ms / 1e3 if ms else None
+
+    def set_comm_timeout(self, ms: int):
+        """crdt_set_comm_timeout: a collective merge's deadline in ms (0 = none).  A host transport given
+        to comm_init_ops that has a ``timeout`` of its own (dist.GlooComm) gets the same bound per operation."""
+        self._check(self._lib.crdt_set_comm_timeout(self._ctx, int(ms)), "crdt_set_comm_timeout")
+        self._comm_timeout_ms = int(ms)
+        comm = getattr(self, "_comm", None)
+        if comm is not None and hasattr(comm, "timeout"):
+            comm.timeout = ms / 1e3 if ms else None
+
+    def comm_state(self) -> tuple[int, str]:
+        """crdt_comm_state: (0 usable / 1 aborted at the deadline / 2 aborted on a transport error, the phase
+        the current or last collective merge is or was in).  Callable from another thread during a merge."""
+        st, ph = ctypes.c_int32(), ctypes.c_char_p()
+        self._check(self._lib.crdt_comm_state(self._ctx, ctypes.byref(st), ctypes.byref(ph)), "crdt_comm_state")
+        return st.value, (ph.value or b"").decode()
 
     def comm_info(self) -> tuple[int, int]:
         n, r = ctypes.c_uint32(), ctypes.c_uint32()

@@ -35,13 +35,30 @@ def attach_rccl(table, dist) -> None:
 class GlooComm:
     """``crdt_comm_ops`` (CRDT_MEM_HOST) over a torch.distributed gloo process group."""
 
-    def __init__(self, dist, group=None):
+    def __init__(self, dist, group=None, timeout: float | None = None):
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self._ops = None
         self.error = None
+        # seconds one operation may take (None: the process group's own timeout).  The library cannot
+        # interrupt a host callback, so a host transport bounds its own operations (include/crdt_merge.h,
+        # crdt_set_comm_timeout); DeviceTable.set_comm_timeout sets it to the library's deadline
+        self.timeout = timeout
+
+    def _wait(self, works) -> None:
+        """Wait for gloo works, all of them within ``timeout`` seconds (a lost or stalled peer raises)."""
+        import datetime
+        import time
+        if self.timeout is None:
+            for w in works:
+                w.wait()
+            return
+        end = time.monotonic() + self.timeout
+        for w in works:
+            left = max(end - time.monotonic(), 1e-3)
+            w.wait(timeout=datetime.timedelta(seconds=left))
 
     # ---- the three operations, on numpy arrays ----------------------------------------
     def all_reduce(self, words: np.ndarray, op: int) -> None:
@@ -49,13 +66,14 @@ class GlooComm:
         t = torch.from_numpy(words)
         red = {REDUCE_SUM: self.dist.ReduceOp.SUM, REDUCE_MAX: self.dist.ReduceOp.MAX,
                REDUCE_MIN: self.dist.ReduceOp.MIN}[op]
-        self.dist.all_reduce(t, op=red, group=self.group)
+        self._wait([self.dist.all_reduce(t, op=red, group=self.group, async_op=True)])
 
     def all_gather(self, send: np.ndarray, recv: np.ndarray) -> None:
         import torch
         n = len(send)
         outs = [torch.from_numpy(recv[r * n:(r + 1) * n]) for r in range(self.world)]
-        self.dist.all_gather(outs, torch.from_numpy(np.ascontiguousarray(send)), group=self.group)
+        self._wait([self.dist.all_gather(outs, torch.from_numpy(np.ascontiguousarray(send)), group=self.group,
+                                         async_op=True)])
 
     def all_to_all_v(self, send_cols, recv_cols, elem_bytes, sc, sd, rc, rd) -> None:
         """Byte columns; to peer d: elements [sd[d], + sc[d]) of every column, from it [rd[d], + rc[d])."""
@@ -71,8 +89,7 @@ class GlooComm:
                 if rc[d]:
                     reqs.append(self.dist.irecv(torch.from_numpy(r[rd[d] * eb:(rd[d] + rc[d]) * eb]), d,
                                                 group=self.group))
-        for q in reqs:
-            q.wait()
+        self._wait(reqs)
 
     # ---- the C table -------------------------------------------------------------------
     def ops(self) -> _capi.CrdtCommOps:

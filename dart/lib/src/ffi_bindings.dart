@@ -99,7 +99,7 @@ typedef _CtxOnlyD = int Function(Pointer<Void>);
 
 const int crdtCommIdBytes = 128;
 /// include/crdt_merge.h CRDT_ABI_VERSION: the struct layouts above are this version's.
-const int crdtAbiVersion = 4;
+const int crdtAbiVersion = 5;
 typedef _AbiC = Int32 Function();
 typedef _AbiD = int Function();
 
@@ -129,7 +129,8 @@ class CrdtLib {
         commInitRccl = lib.lookupFunction<_CommInitC, _CommInitD>('crdt_comm_init_rccl'),
         commInfo = lib.lookupFunction<_CommInfoC, _CommInfoD>('crdt_comm_info'),
         commFree = lib.lookupFunction<_CtxOnlyC, _CtxOnlyD>('crdt_comm_free'),
-        setPresharded = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_presharded');
+        setPresharded = lib.lookupFunction<_CtxIntC, _CtxIntD>('crdt_set_presharded'),
+        setCommTimeout = lib.lookupFunction<_CtxU32C, _CtxIntD>('crdt_set_comm_timeout');
 
   /// Opens the library and refuses one built against another ABI (crdt_timing / crdt_result layouts).
   factory CrdtLib.open([String path = 'libcrdt_mi355x.so']) {
@@ -164,6 +165,9 @@ class CrdtLib {
   final _CommInitD commInitRccl;
   final _CommInfoD commInfo;
   final _CtxOnlyD commFree;
+  /// crdt_set_comm_timeout: a collective merge's deadline (ms; 0 = none) — past it the communicator is
+  /// aborted and the merge throws (CRDT_E_COMM) instead of waiting forever on a lost peer.
+  final _CtxIntD setCommTimeout;
   final _CtxIntD setPresharded;
 }
 

@@ -114,7 +114,8 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
         _hostPath = hostLibrary,
         _nRanks = 1,
         _shardRank = 0,
-        _commId = null {
+        _commId = null,
+        _commTimeoutMs = 0 {
     // (the base constructor has already run refreshCanonicalTime() on the empty map: 0)
     if (seed.isNotEmpty) _store(seed, notify: false); // map_crdt.dart:16-18: no clock refresh
   }
@@ -139,6 +140,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
       required Uint8List commId,
       int device = 0,
       int capacity = 1024,
+      int commTimeoutMs = 300000,
       String? library,
       String? hostLibrary})
       : _lib = CrdtLib.open(library ?? 'libcrdt_mi355x.so'),
@@ -147,7 +149,8 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
         _hostPath = hostLibrary,
         _nRanks = nRanks,
         _shardRank = rank,
-        _commId = commId {
+        _commId = commId,
+        _commTimeoutMs = commTimeoutMs {
     if (commId.length != crdtCommIdBytes) throw ArgumentError.value(commId.length, 'commId', 'must be 128 bytes');
     _c; // join the communicator now: every rank constructs its shard together
   }
@@ -167,6 +170,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
 
   final int _nRanks;
   final int _shardRank;
+  final int _commTimeoutMs; // a collective merge's deadline in ms (crdt_set_comm_timeout; 0: none)
   final Uint8List? _commId;
   bool get _sharded => _commId != null;
 
@@ -214,6 +218,7 @@ class GpuMapCrdt<K, V> extends Crdt<K, V> {
           try {
             id.asTypedList(crdtCommIdBytes).setAll(0, _commId!);
             _check(_lib.commInitRccl(_ctx, _nRanks, _shardRank, id), 'crdt_comm_init_rccl');
+            _check(_lib.setCommTimeout(_ctx, _commTimeoutMs), 'crdt_set_comm_timeout');
             _check(_lib.setPresharded(_ctx, 1), 'crdt_set_presharded'); // key ids are this shard's slots
           } finally {
             calloc.free(id);

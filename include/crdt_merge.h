@@ -38,8 +38,9 @@
 extern "C" {
 #endif
 
-#define CRDT_ABI_VERSION 4          /* 3: crdt_timing gained part1_records (round 3); 4: crdt_route_tune_info
-                                       reports five ways, crdt_timing gained sent_bytes (round 5) */
+#define CRDT_ABI_VERSION 5          /* 3: crdt_timing gained part1_records (round 3); 4: crdt_route_tune_info
+                                       reports five ways, crdt_timing gained sent_bytes (round 5); 5: the
+                                       collective deadline, crdt_set_comm_timeout / crdt_comm_state (round 6) */
 #define CRDT_NULL_VALUE 0xFFFFFFFFu
 
 /* Status codes.  1..3 mirror the reference exceptions (hlc.dart:164-189); the
@@ -209,13 +210,20 @@ int crdt_merge(crdt_ctx* ctx, const crdt_batch* batch, int64_t wall_millis, uint
  *   6. SUM all-reduce of the per-record counts and of the key-range error.
  * Every rank returns the same status, stop point, canonical and counts; win_flags
  * (optional, [n] of the local batch) come back to the rank that passed the record.
- * A failure local to one rank (CRDT_E_NOMEM, CRDT_E_INVALID of its own batch, CRDT_E_HIP)
- * is carried through the call's collectives and returned by EVERY rank — no rank is left
- * waiting in a collective its peers will not post.  Before the record exchange nothing is
- * stored and the canonical clock does not move; a failure in the owners' apply (after the
- * exchange) leaves the other ranks' rows of the stopped call stored and the canonical
- * unchanged (re-merging the same batch is exact).  Rank-local still: a failing transport
- * (CRDT_E_COMM) and a rank that cannot allocate the call's O(R) gather words.
+ * A failure local to one rank (CRDT_E_NOMEM, CRDT_E_INVALID of its own batch, CRDT_E_HIP
+ * of a launch or copy) is carried through the call's collectives and returned by EVERY
+ * rank — no rank is left waiting in a collective its peers will not post.  Before the
+ * record exchange nothing is stored and the canonical clock does not move; a failure in the
+ * owners' apply (after the exchange) leaves the other ranks' rows of the stopped call stored
+ * and the canonical unchanged (re-merging the same batch is exact).  Rank-local still: a
+ * failing transport, a rank that cannot allocate the call's O(R) gather words, and a HIP
+ * failure of a read-back of agreed words (without them the rank cannot post what its peers
+ * post next).  Those — and a peer that died, hung or faulted — end at the call's DEADLINE:
+ * every host wait of a sharded call polls against it (crdt_set_comm_timeout); past it the
+ * communicator is aborted (ncclCommAbort for RCCL) and the call returns CRDT_E_COMM.  After
+ * CRDT_E_COMM the ctx refuses sharded merges (CRDT_E_COMM) until it joins a communicator
+ * again (crdt_comm_free + crdt_comm_init_*), and the rows of its shard the failed call may
+ * have touched are undefined (re-sync the shard).
  * Keys in the batch are GLOBAL key ids, unless crdt_set_presharded(ctx, 1): then every
  * record is already on its owner and key_id holds its slot (no record exchange).
  *
@@ -251,6 +259,18 @@ int crdt_comm_init_rccl(crdt_ctx* ctx, uint32_t n_ranks, uint32_t rank, const ui
 int crdt_comm_init_ops(crdt_ctx* ctx, uint32_t n_ranks, uint32_t rank, const crdt_comm_ops* ops);
 int crdt_comm_info(const crdt_ctx* ctx, uint32_t* n_ranks, uint32_t* rank);
 int crdt_comm_free(crdt_ctx* ctx);
+/* The deadline of one collective crdt_merge, in ms from the call's entry (default 300000, or the
+ * CRDT_COMM_TIMEOUT_MS environment variable at crdt_create; 0 = wait forever).  With RCCL every
+ * host wait of the call polls the device against it and against ncclCommGetAsyncError; past it
+ * the communicator is aborted and the call returns CRDT_E_COMM.  A CRDT_MEM_HOST transport blocks
+ * inside its callbacks and must bound each operation itself (e.g. its own timeout); a callback
+ * that fails, or returns after the deadline, fails the call the same way. */
+int crdt_set_comm_timeout(crdt_ctx* ctx, uint32_t ms);
+/* *state: 0 = the communicator is usable, 1 = aborted at a deadline, 2 = aborted on a transport
+ * error; *phase: where the current or last collective merge is or was (static text, e.g.
+ * "route_l1: record exchange").  Safe to call from another thread while crdt_merge runs (a
+ * watchdog's report); the pointer stays valid for the process's life. */
+int crdt_comm_state(const crdt_ctx* ctx, int32_t* state, const char** phase);
 /* presharded = 1: batches hold only records this rank owns, key_id = slot (no exchange) */
 int crdt_set_presharded(crdt_ctx* ctx, int presharded);
 

@@ -150,3 +150,66 @@ def test_home_part_layout():
     assert sel.tolist() == [0, 1, 2, 5, 6, 7, 8] and offs.tolist() == [0, 3, 3, 7]
     sel, offs = home_part(np.array([0, 3, 5, 9], np.uint64), 2, 1)
     assert sel.tolist() == [3, 4] and offs.tolist() == [0, 0, 2, 2]
+
+
+# ---- a host transport bounds its own operations (crdt_set_comm_timeout) ------------------
+def _timeout_worker(rank, world, port, q, what):
+    import datetime
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    comm = GlooComm(dist, timeout=1.0)
+    dist.barrier()
+    if rank == world - 1:                       # the stalled (or lost) peer
+        if what == "exit":
+            os._exit(17)
+        time.sleep(5.0)
+    words = np.zeros(4, np.int64)
+    t0 = time.monotonic()
+    try:
+        {"reduce": lambda: comm.all_reduce(words, 1),
+         "gather": lambda: comm.all_gather(words, np.zeros(4 * world, np.int64)),
+         "exit": lambda: comm.all_reduce(words, 1),
+         "a2a": lambda: comm.all_to_all_v([np.zeros(8 * world, np.uint8)], [np.zeros(8 * world, np.uint8)], [1],
+                                          [0 if d == rank else 8 for d in range(world)], [8 * d for d in range(world)],
+                                          [0 if d == rank else 8 for d in range(world)], [8 * d for d in range(world)])}[what]()
+        err = None
+    except Exception as e:  # noqa: BLE001 -- the timeout surfaces as the transport's error
+        err = type(e).__name__
+    q.put((rank, err, time.monotonic() - t0))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("what,world", [("reduce", 2), ("gather", 3), ("a2a", 2), ("exit", 3)])
+def test_gloo_comm_timeout_bounds_each_operation(what, world):
+    """GlooComm(timeout=1 s): an operation whose peer stalls (or exited) raises on the waiting ranks within
+    the bound — the error the library turns into CRDT_E_COMM — instead of blocking until the peer returns."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, world, port, q, what)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(world - 1)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=30)
+    for rank, err, el in outs:
+        if rank == world - 1:
+            continue
+        assert err is not None, (rank, el)
+        assert el < 4.0, (rank, el)             # the stalled peer slept 5 s: the bound ended the wait
+
+
+def test_bench_watchdog_reports_and_exits():
+    """bench.py's per-rank watchdog: a call that overruns its bound prints the rank's phase and exits 4."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import time, bench; w = bench.Watchdog(3); w.arm(10, 'early'); w.disarm(); "
+            "w.arm(0.6, 'merge step (merging)'); time.sleep(10); print('not reached')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 4, (r.returncode, r.stderr[-500:])
+    assert "rank 3: WATCHDOG: merge step (merging) overran" in r.stderr, r.stderr[-500:]
+    assert "not reached" not in r.stdout

@@ -117,7 +117,7 @@ def test_library_exports_every_header_symbol():
     assert declared <= exported, declared - exported
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.crdt_abi_version() == _capi.ABI_VERSION == 4
+    assert lib.crdt_abi_version() == _capi.ABI_VERSION == 5
     assert _capi.status_string(1) == "clock drift"
 
 
