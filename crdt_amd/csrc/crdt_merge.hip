@@ -141,7 +141,8 @@ struct Misc {
                                     // bit 2 (k_shard_combine) = the ranks' collective-shape words differ
     unsigned long long shard_status; // k_shard_combine: the largest local failure code (-CRDT_E_*) any rank put in
                                      // its gather row (0: none) — every rank fails the call with it
-    unsigned long long pad_;
+    unsigned long long fr_cmax;      // k_scan<.., kFrame>: max of the records' lt & 0xFFFF (the compact frame,
+                                     // sorted_path.inc PackFrame::cb)
     unsigned long long present[kCounterSlots];
     unsigned long long won[kCounterSlots];
 };                             // size a multiple of 16 B: hipMemsetAsync zeroes it with one fill
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     // (kFrame without kEager: the lt frame only — the host declared a rank bound, crdt_set_rank_bound)
     __shared__ int64_t s_max[kScanThreads / 64];
     __shared__ int s_flag[kScanThreads / 64];
-    __shared__ unsigned long long s_fr[kFrame ? 4 * (kScanThreads / 64) : 1];
+    __shared__ unsigned long long s_fr[kFrame ? 5 * (kScanThreads / 64) : 1];
     __shared__ uint32_t s_h[kHist ? 512 : 1];
     static_assert(!kHist || kScanThreads == 256, "one histogram bin per thread");
     const uint32_t j = jbase + blockIdx.y;
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
             }
         }
         unsigned long long flo = 0, fhi = 0, frl = 0, frh = 0;   // max-accumulators (0: none)
+        uint32_t fcm = 0;                                          // max lt & 0xFFFF (the compact frame)
         if (kFrame) {
 #pragma unroll
             for (int q = 0; q < kScanItems; ++q) {
@@ -359,6 +361,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                     const uint64_t o = ord64(v[q]);
                     flo = ~o > flo ? ~o : flo;
                     fhi = o > fhi ? o : fhi;
+                    fcm = std::max<uint32_t>(fcm, (uint32_t)v[q] & 0xFFFFu);
                     if (kEager) {
                         const uint32_t r = rk[kEager ? q : 0];
                         frl = (uint32_t)~r > frl ? (uint32_t)~r : frl;
@@ -371,8 +374,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                 const unsigned long long a = __shfl_xor(flo, off, 64), b = __shfl_xor(fhi, off, 64);
                 const unsigned long long c = __shfl_xor(frl, off, 64), d = __shfl_xor(frh, off, 64);
                 flo = a > flo ? a : flo; fhi = b > fhi ? b : fhi; frl = c > frl ? c : frl; frh = d > frh ? d : frh;
+                fcm = std::max<uint32_t>(fcm, (uint32_t)__shfl_xor(fcm, off, 64));
             }
-            if (lane == 0) { s_fr[4 * w] = flo; s_fr[4 * w + 1] = fhi; s_fr[4 * w + 2] = frl; s_fr[4 * w + 3] = frh; }
+            if (lane == 0) {
+                s_fr[5 * w] = flo; s_fr[5 * w + 1] = fhi; s_fr[5 * w + 2] = frl; s_fr[5 * w + 3] = frh; s_fr[5 * w + 4] = fcm;
+            }
         }
         m = wave_max(m);
         const int fw = __any(f) | (m > c0 ? 2 : 0);
@@ -380,12 +386,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
         __syncthreads();
         if (threadIdx.x == 0) {
             if (kFrame) {
+                unsigned long long fc = fcm;
                 for (int k = 1; k < kScanThreads / 64; ++k) {
-                    flo = s_fr[4 * k] > flo ? s_fr[4 * k] : flo;
-                    fhi = s_fr[4 * k + 1] > fhi ? s_fr[4 * k + 1] : fhi;
-                    frl = s_fr[4 * k + 2] > frl ? s_fr[4 * k + 2] : frl;
-                    frh = s_fr[4 * k + 3] > frh ? s_fr[4 * k + 3] : frh;
+                    flo = s_fr[5 * k] > flo ? s_fr[5 * k] : flo;
+                    fhi = s_fr[5 * k + 1] > fhi ? s_fr[5 * k + 1] : fhi;
+                    frl = s_fr[5 * k + 2] > frl ? s_fr[5 * k + 2] : frl;
+                    frh = s_fr[5 * k + 3] > frh ? s_fr[5 * k + 3] : frh;
+                    fc = s_fr[5 * k + 4] > fc ? s_fr[5 * k + 4] : fc;
                 }
+                if (fc > *(volatile unsigned long long*)&misc->fr_cmax) atomicMax(&misc->fr_cmax, fc);
                 if (flo > *(volatile unsigned long long*)&misc->fr_lo) atomicMax(&misc->fr_lo, flo);
                 if (fhi > *(volatile unsigned long long*)&misc->fr_hi) atomicMax(&misc->fr_hi, fhi);
                 if ((uint32_t)frl > *(volatile uint32_t*)&misc->fr_rlo) atomicMax(&misc->fr_rlo, (uint32_t)frl);
@@ -1064,7 +1073,7 @@ __global__ __launch_bounds__(256) void k_unpack_routed(int64_t* __restrict__ lt,
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t x = (uint64_t)lt[i];
-    lt[i] = (int64_t)((uint64_t)pf.lt0 + (x >> pf.sh));
+    lt[i] = pack_lt(pf, x);
     rank[i] = pack_rank(pf, x);
 }
 
@@ -1532,9 +1541,13 @@ constexpr uint32_t kFormNoVecScan = 32768;   // the scan (with the level-1 histo
 constexpr uint32_t kFormNoVecRoute = 131072; // routing kernels: strided loads, one LDS atomic per record
 constexpr uint32_t kFormBigTile2 = 65536;    // level-2 tiles of 32K records (not 8K)
 constexpr uint32_t kFormNoOwnInPlace = 524288; // sharded merge: the own chunk copied to the receive columns
-constexpr uint32_t kFormNoFbackXcd = 1u << 21;   // flag passes: plain tile order (not the scatters' XCD order)
-constexpr uint32_t kFormNoFbackWide = 1u << 22;  // flag passes: one staged byte per load (CRDT_FBACK_CHK applies)
-constexpr uint32_t kFormNoOverlap = 1u << 23;    // sorted path: split buckets' fold / carry not beside the resolve
+// round 6, measured slower and kept as opt-in forms: the flag passes in the scatters' XCD tile order,
+// and with four-byte staging + eight-record gathers (CRDT_FBACK_CHK applies to the default byte staging only)
+constexpr uint32_t kFormNoCompact = 1u << 20;   // no compact form (PackFrame::cb): 14-B / 13-B partition records
+constexpr uint32_t kFormFbackXcd = 1u << 21;
+constexpr uint32_t kFormFbackWide = 1u << 22;
+constexpr uint32_t kFormOverlap = 1u << 23;      // sorted path: split buckets' fold / carry beside the unsplit
+                                                 // buckets' resolve (measured slower: opt-in)
 constexpr uint32_t kPartPad = 1024;          // records of slack behind every partition buffer (tile-end vector loads)
 constexpr uint32_t kPutGrid = 2048;          // k_put_rows / k_put_stamped workgroups (grid-stride)
 
@@ -1647,6 +1660,7 @@ struct crdt_ctx {
     bool last_own_in_place = false; // ... and scattered its own chunk into the receive columns
     bool last_key8 = false;         // ... with 1-B final key columns
     bool last_key16 = false;        // ... and 2-B level-1 key columns
+    bool last_compact = false;      // ... in the compact form (12-B records; PackFrame::cb)
     bool last_hw = false;           // ... whose packed resolve skipped the rows >= hw_read
     // per-record win flags on the sorted path (the flagged form, sorted_path.inc): CRDT_FLAGS_SORTED=0
     // keeps every flagged merge on the gather path
@@ -2406,6 +2420,20 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     // final records with a 1-B key column when the packed key leaves 4 bits free (two levels)
     const bool k8 = pk && two && pf.key4 && !(c->form_off & kFormNoKey8);
     const bool k16 = k8 && !(c->form_off & kFormNoKey16);     // ... and 2-B level-1 key columns
+    // the compact form (round 6; sorted_path.inc PackFrame::cb): on one ctx's order-free packed form, when the
+    // records' lt & 0xFFFF (the scan's fr_cmax) leave the lt field short enough, 12-B records that carry their
+    // whole 20-bit level-1 slot (+ a 1-B level-2 digit column at level 1) instead of 14 + 13 B
+    bool cmp = false;
+    if (k16 && (ord || !c->counts) && !em && !c->has_comm && !cols.packed_in && c->frame_on &&
+        !(c->form_off & (kFormNoCompact | kFormNoHistW | kFormBigTile2 | kFormNoWholeLines | kFormNoVecLoads))) {
+        const PackFrame cf = compact_frame(pf, (uint32_t)std::min<unsigned long long>(c->h_misc->fr_cmax, 0xFFFFull),
+                                           c->plan_R);
+        if (cf.cb) {
+            pf = cf;
+            cmp = true;
+        }
+    }
+    c->last_compact = cmp;
     c->last_key8 = k8;
     c->last_key16 = k16;
     c->last_hw = pk && (!c->counts || ord) && c->hw_read < c->cap;     // (in the first window)
@@ -2528,7 +2556,17 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));   // (the first window)
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
-        if (fl && k16)          // the flagged form: each record's level-1 position kept at its input index
+        if (cmp && fl)          // the compact form's flagged level 1 (with positions)
+            k_part_scatter1<true, false, true, kL1Items, true, true, true, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, c->f_pos1.p, hist1);
+        else if (cmp)           // the compact form: 12-B records + the 1-B level-2 digit column
+            k_part_scatter1<true, false, true, kL1Items, true, true, false, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr);
+        else if (fl && k16)     // the flagged form: each record's level-1 position kept at its input index
             k_part_scatter1<true, false, true, kL1Items, true, true, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
@@ -2598,7 +2636,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             tm2f = tm2;
             nt2f = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const ScanMap sm2{tb2, cb2, c->p_l1beg.p, kDigits};
-            if (k16 && !(c->form_off & kFormNoHistW) && ts2 == (uint32_t)kPTile2)   // key bits [4, 20) in 2 B:
+            if (cmp)                                     // the compact form's 1-B level-2 digits
+                k_part_hist16w<256, kPTile2, true><<<nt2, 256, 0, c->stream>>>(
+                    reinterpret_cast<const uint16_t*>(p1k), tm2, 0, h2p);
+            else if (k16 && !(c->form_off & kFormNoHistW) && ts2 == (uint32_t)kPTile2)   // key bits [4, 20) in 2 B:
                 k_part_hist16w<256, kPTile2><<<nt2, 256, 0, c->stream>>>(   // the level-2 digit (bits [12, 20))
                     reinterpret_cast<const uint16_t*>(p1k), tm2, kSBits - 4, h2p);   // is its high byte
             else if (k16 && !(c->form_off & kFormNoHistW))
@@ -2624,7 +2665,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 const Rec12* i12 = reinterpret_cast<const Rec12*>(p1r);
                 Rec12* o12 = reinterpret_cast<Rec12*>(p2r);
                 const uint32_t jm = (uint32_t)pack_jmask(pf);
-                if (k16)
+                if (cmp)
+                    k_part_scatter2_seg<true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        i12, nullptr, tm2, 24, t2p, o12, nullptr, xper2, jm, pos2, h2p);
+                else if (k16)
                     k_part_scatter2_seg<true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         i12, p1k, tm2, kSBits - 4, t2p, o12, p2k, xper2, jm, pos2, h2p);
                 else if (k8)
@@ -2637,7 +2681,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_part_scatter2<true, false><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                     p1r, p1k, tm2, kSBits, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
             else if (pk)
-                if (k16)
+                if (cmp)       // (the record moves as it is: its digit is the word's top byte)
+                    k_part_scatter2<false, true, true, true, true, true>
+                        <<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
+                        p1r, nullptr, tm2, 24, t2p, p2r, nullptr, xper2, rev1 ? h2p : nullptr);
+                else if (k16)
                     k_part_scatter2<false, true, true, true><<<xcd_grid(nt2s, c->xcd_map), kPThreads, 0, c->stream>>>(
                         p1r, p1k, tm2, kSBits - 4, t2p, p2r, p2k, xper2, rev1 ? h2p : nullptr);
                 else if (k8)
@@ -2669,7 +2717,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         KeyState cy{c->p_kslt.p + ksn, c->p_ksu32.p + 3 * ksn, c->p_ksu32.p + 4 * ksn, c->p_ksu32.p + 5 * ksn};
         HIPALLOC(c->p_ibucket.ensure(max_items));
         // split buckets (parts folded apart, then carried) beside the unsplit buckets' resolve: two streams
-        const bool ov = !em && pk && (ord || !c->counts) && two && !(c->form_off & kFormNoOverlap);
+        const bool ov = !em && pk && (ord || !c->counts) && two && (c->form_off & kFormOverlap);
         if (ph) ev_record(c, ev_window(3, false));
         if (em) HIPALLOC(c->e_bbase.ensure(nb));
         k_bucket_items<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, c->d_misc,
@@ -2729,7 +2777,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             int st = ov ? overlap_fork(c) : CRDT_OK;
             if (st) return st;
             const hipStream_t fs = ov ? c->sstream : c->stream;
-            if (k8)
+            if (cmp)
+                k_resolve_packed<true, true, false, false, true><<<max_items, kQThreads, 0, fs>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                    ps_key, ps_val, pf, c->d_misc);
+            else if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
                     ps_val, pf, c->d_misc);
@@ -2743,7 +2795,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
             for (uint32_t which = ov ? 1u : 0u; which <= (ov ? 2u : 0u); ++which) {
                 if (which == 2 && (st = overlap_join(c))) return st;
-                if (k8)
+                if (cmp)
+                    k_resolve_pflags<false, true><<<max_items, kRThreads, 0, c->stream>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p,
+                        jb, cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
+                else if (k8)
                     k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
                         bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
                         cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
@@ -2756,7 +2812,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint8_t* f1 = c->f_flag2.p;
             if (fl && two) {
                 HIPALLOC(c->f_flag1.ensure(nw + 8));
-                const bool fx = c->xcd_map && !(c->form_off & kFormNoFbackXcd);
+                const bool fx = c->xcd_map && (c->form_off & kFormFbackXcd);
                 const uint32_t xf2 = fx ? (nt2f + kXcds - 1) / kXcds : 0;
 #define CRDT_FBACK2(CHK, W)                                                                               \
     if (tm2f.tsize == (uint32_t)kPTile2)                                                                  \
@@ -2765,7 +2821,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     else                                                                                                  \
         k_flags_back<false, CHK, kPTile, W><<<xcd_grid(nt2f, fx), 512, 0, c->stream>>>(                   \
             tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc, xf2)
-                if (!(c->form_off & kFormNoFbackWide)) { CRDT_FBACK2(6, true); }
+                if (c->form_off & kFormFbackWide) { CRDT_FBACK2(6, true); }
                 else if (c->fback_chk == 4) { CRDT_FBACK2(4, false); }
                 else if (c->fback_chk == 6) { CRDT_FBACK2(6, false); }
                 else { CRDT_FBACK2(0, false); }
@@ -2775,13 +2831,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                 k_seg_index<<<std::min<uint32_t>(grid_for(nt1, 256), 4096), 256, 0, c->stream>>>(d_tb1, nseg, nt1,
                                                                                                  c->p_tseg.p);
             }
-            const bool fx1 = c->xcd_map && !(c->form_off & kFormNoFbackXcd);
+            const bool fx1 = c->xcd_map && (c->form_off & kFormFbackXcd);
             const uint32_t xf1 = fx1 ? (nt1 + kXcds - 1) / kXcds : 0;
 #define CRDT_FBACK1(CHK, W)                                                                               \
     k_flags_back<true, CHK, kPTile, W><<<xcd_grid(nt1, fx1), 512, 0, c->stream>>>(                        \
         tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc, xf1)
             if (fl) {
-                if (!(c->form_off & kFormNoFbackWide)) { CRDT_FBACK1(6, true); }
+                if (c->form_off & kFormFbackWide) { CRDT_FBACK1(6, true); }
                 else if (c->fback_chk == 4) { CRDT_FBACK1(4, false); }
                 else if (c->fback_chk == 6) { CRDT_FBACK1(6, false); }
                 else { CRDT_FBACK1(0, false); }
@@ -2803,7 +2859,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             int st = ov ? overlap_fork(c) : CRDT_OK;
             if (st) return st;
             const hipStream_t fs = ov ? c->sstream : c->stream;
-            if (k8)
+            if (cmp)
+                k_resolve_packed<true, true, false, false, true><<<max_items, kQThreads, 0, fs>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                    ps_key, ps_val, pf, c->d_misc);
+            else if (k8)
                 k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
@@ -2813,7 +2873,11 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                     pf, c->d_misc);
             k_part_carry_packed<false><<<dim3(kSKeys / 256, max_hot), 256, 0, fs>>>(
                 d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
-            if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
+            if (cmp)
+                k_resolve_packed<false, true, false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
+                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                    ps_key, ps_val, pf, c->d_misc, EmitOut{}, c->sparse_t);
+            else if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
                 k_resolve_packed<false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
@@ -3518,6 +3582,7 @@ int crdt_last_plan(const crdt_ctx* c, uint32_t* flags) {
         if (c->last_ordered) f |= CRDT_PLAN_ORDERED;
         if (c->last_combined) f |= CRDT_PLAN_COMBINED;
         if (c->last_route_l1) f |= CRDT_PLAN_ROUTE_L1;
+        if (c->last_compact) f |= CRDT_PLAN_COMPACT;
     }
     if (c->last_wire_pk) f |= CRDT_PLAN_WIRE_PACKED;
     if (c->last_own_in_place) f |= CRDT_PLAN_OWN_IN_PLACE;

@@ -331,7 +331,8 @@ class DeviceTable:
     PLAN_FLAGS = {"sorted": 1, "packed": 2, "two_level": 4, "hist_in_scan": 8, "key8": 16, "key16": 32,
                   "high_water": 64, "anchored": 128, "wire_packed": 256, "own_in_place": 512,
                   "flagged": 1024, "ordered": 2048,
-                  "combined": 4096, "route_l1": 8192, "route_tuned": 16384, "rl1_head": 262144}
+                  "combined": 4096, "route_l1": 8192, "route_tuned": 16384, "rl1_head": 262144,
+                  "compact": 524288}
 
     def last_plan(self) -> dict:
         """crdt_last_plan: how the last merge ran ({'sorted': bool, 'packed': ..., ...})."""

@@ -330,9 +330,13 @@ enum crdt_plan_flags {
     CRDT_PLAN_ROUTE_TUNED = 16384, /* sharded ctx: the way (route_l1 or the combine) came from the routing
                                     tuner, a trial or its measured choice (crdt_route_tune_info) */
     CRDT_PLAN_RL1_PIECES_SHIFT = 15, /* bits 15-17: route_l1's pipelined pieces (1-4; 0: not route_l1) */
-    CRDT_PLAN_RL1_HEAD = 262144  /* route_l1 folded each owner's first level-1 digit (its 2^20 lowest slots,
+    CRDT_PLAN_RL1_HEAD = 262144, /* route_l1 folded each owner's first level-1 digit (its 2^20 lowest slots,
                                     the Zipf head) at the sender: one packed maximum per key crossed the
                                     exchange for those keys (comm_path.inc) */
+    CRDT_PLAN_COMPACT = 524288   /* the sorted path's compact form: the records' lt field packed as
+                                    (lt >> 16 - min, lt & 0xFFFF) in as many bits as the batch needs, so a record's
+                                    whole 20-bit level-1 slot rides in its 64-bit key: 12-B partition records
+                                    (sorted_path.inc, PackFrame::cb) */
 };
 int crdt_last_plan(const crdt_ctx* ctx, uint32_t* flags);
 

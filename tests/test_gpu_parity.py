@@ -1098,7 +1098,8 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
     t.close()
 
 
-@pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536"])
+@pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536",
+                                      "8388608"])
 def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
@@ -1109,7 +1110,8 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
-    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536")), res["plan"]
+    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536", "8388608")), \
+        res["plan"]
 
 
 @pytest.mark.parametrize("sparse_t", ["0", "1024", "1000000000"])
@@ -1783,12 +1785,17 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
     assert res["path"] == "gather" and not res["plan"]["flagged"]
 
 
-@pytest.mark.parametrize("chk", ["0", "4", "6"])
-def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk):
-    """The flag passes' run search without checkpoints (CRDT_FBACK_CHK=0), with one per 16 staged
-    bytes (4) and one per 64 (6, the default): split hot bucket, cold buckets on the 2-B level-1 key
-    column, a late drift — same flags, rows and counts as the oracle."""
+@pytest.mark.parametrize("chk,form", [("0", "0"), ("4", "0"), ("6", "0"), ("6", "4194304"), ("6", "2097152"),
+                                      ("6", "8388608"), ("6", "14680064")])
+def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, form):
+    """The flag passes: the one-byte staging with its run search without checkpoints (CRDT_FBACK_CHK=0), one
+    per 16 staged bytes (4) and one per 64 (6, the default); the opt-in forms of CRDT_SORTED_FORM: four-byte
+    staging with eight-record gathers (4194304), the scatters' XCD tile order (2097152), the split buckets' fold
+    and carry-ins on a side stream beside the unsplit buckets' walk (8388608), all three (14680064): split hot
+    bucket, cold buckets on the 2-B level-1 key column, a late drift — same flags, rows and counts as the
+    oracle."""
     monkeypatch.setenv("CRDT_FBACK_CHK", chk)
+    monkeypatch.setenv("CRDT_SORTED_FORM", form)
     case = make_case(seed=85, R=120, per_cs=2000, n_local=3000, n_new=1000, millis_span=4, counter_span=3,
                      n_ranks=9, tomb_frac=0.2, neg_mod_frac=0.05)
     assert _flagged(case, _TWO)["plan"]["flagged"]
@@ -1835,3 +1842,86 @@ def test_flagged_equals_gather_fanin(gpu_device, K, total, R):
     for a, b in zip(ag, as_):
         assert np.array_equal(a, b)
     torch.cuda.empty_cache()
+
+
+# ---- the compact form (round 6; sorted_path.inc PackFrame::cb, CRDT_PLAN_COMPACT) --------------------------
+def _compact_edge_case(seed, cmax=14, wall=None, explicit_millis=False, millis_span=6):
+    """Records whose lt & 0xFFFF reach cmax (14: cb = 4, the top field value 15 reserved), local rows at every
+    edge of the compact lt field: counters cmax, cmax + 1 (= the reserved top), cmax + 2 and 0xFFFF at millis
+    inside the frame (packed as the top: above every record of their millis, below the next), rows just below /
+    above the frame, exact copies of records (equal (lt, rank): local keeps)."""
+    from tests._cases import WALL
+    case = make_case(seed=seed, R=48, per_cs=2500, n_local=4000, n_new=1500, millis_span=millis_span,
+                     counter_span=cmax + 1, base=(WALL if wall is None else wall) - millis_span - 1000,
+                     n_ranks=9, local_rank=0, tomb_frac=0.2, wall=WALL if wall is None else wall,
+                     explicit_millis=explicit_millis)
+    rng = np.random.default_rng(seed)
+    lo, hi = int(case["lt"].min()), int(case["lt"].max())
+    loc = case["local"]
+    n = case["n_local"]
+    ms = rng.integers(lo >> 16, (hi >> 16) + 1, n)
+    cnt = np.array([0, cmax, cmax + 1, cmax + 2, 0xFFFF], np.int64)[rng.integers(0, 5, n)]
+    lt = (ms << 16) + cnt
+    edge = rng.random(n)
+    lt = np.where(edge < 0.05, lo - 1, np.where(edge > 0.95, hi + 1, lt))
+    loc["lt"] = lt.astype(np.int64)
+    first = {}
+    for x, k in enumerate(case["key"].tolist()):
+        first.setdefault(k, x)
+    for k in rng.choice(n, n // 10, replace=False):
+        if int(k) in first:
+            loc["lt"][k] = case["lt"][first[int(k)]]
+            loc["rank"][k] = case["rank"][first[int(k)]]
+    loc["mod"] = np.where(loc["mod"] >= 0, loc["lt"], loc["mod"])
+    vis = loc["mod"] >= 0
+    case["c0"] = int(loc["lt"][vis].max())
+    return case
+
+
+@pytest.mark.parametrize("form", ["0", "1048576"])
+@pytest.mark.parametrize("variant", ["cmax14", "cmax0", "cmax200", "wide_span", "explicit_millis", "no_fit"])
+def test_sorted_compact_form(gpu_device, monkeypatch, form, variant):
+    """The compact lt field (CRDT_SORTED_FORM 1048576 switches it off: the 14-B / 13-B records): the same rows,
+    canonical and exception fields as the oracle on two-level tables, with local rows at every edge of the
+    compact field; and the plan reports which form ran."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", form)
+    kw = {"cmax14": {}, "cmax0": {"cmax": 0}, "cmax200": {"cmax": 200},
+          "wide_span": {"millis_span": 1 << 20}, "explicit_millis": {"explicit_millis": True},
+          "no_fit": {"millis_span": 1 << 20, "cmax": 60000}}[variant]     # (no_fit: 20 + 16 bits: the plain field)
+    case = _compact_edge_case(77, **kw)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
+                              rank_bound=int(case["rank"].max()) + 1, device_cols=True)
+    assert res["plan"]["packed"] and res["plan"]["two_level"]
+    assert res["plan"]["compact"] == (form == "0" and variant != "no_fit"), res["plan"]
+
+
+def test_sorted_compact_fanin_equals_oracle(gpu_device):
+    """A fan-in shape (gen_fanin: 2^16 ms of clocks, counters < 16 — the bench's) takes the compact form and
+    leaves exactly the C oracle's rows; switched off, the same rows."""
+    import os
+
+    from crdt_amd import DeviceTable
+    from crdt_amd.workload import gen_fanin
+    K, total, R = 1 << 22, 3_000_000, 64
+    ref, rows = _fanin_reference(K, total, R)
+    wl = gen_fanin(total=total, R=R, K=K, n_local=K // 2, s=0.8, device="cuda")
+    loc, own = wl["local"], wl["owned"]
+    for form in ("0", "1048576"):
+        os.environ["CRDT_SORTED_FORM"] = form
+        try:
+            t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
+            t.set_counts(False)
+            t.set_merge_path("sorted")
+            t.set_rank_bound(R + 1)
+            t.put_rows(loc["slot"], loc["lt"], loc["rank"], loc["val"], loc["mod"])
+            t.canonical = wl["c0"]
+            res, _ = t.merge(own["key"], own["lt"], own["rank"], own["val"], wl["owned_offsets"], wl["wall"],
+                             win_flags=False)
+            assert t.last_plan()["compact"] == (form == "0"), t.last_plan()
+            for f in ("status", "n_stored", "canonical_lt"):
+                assert res[f] == ref[f], (form, f)
+            for a, b in zip(t.read_rows(np.arange(wl["capacity"], dtype=np.uint32)), rows):
+                assert np.array_equal(a, b), form
+            t.close()
+        finally:
+            os.environ.pop("CRDT_SORTED_FORM", None)

@@ -14,6 +14,49 @@ case "${STAGE:-comm}" in
     timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "rccl" > gpurun_out/${TAG}_pytest_rccl.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_rccl.log; exit 1; }
     tail -2 gpurun_out/${TAG}_pytest_rccl.log ;;
+  perf1)
+    # sorted / flagged parity subset (the new flag-pass staging, XCD order, the two-stream resolve), then in-process
+    # A/Bs: the order-free step (overlap on / off), the flagged merge (new forms vs the old ones), cfg3
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "sorted or flagged" > gpurun_out/${TAG}_pytest_sorted.log 2>&1 \
+      || { tail -40 gpurun_out/${TAG}_pytest_sorted.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_sorted.log
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --ab CRDT_SORTED_FORM=0,8388608 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_overlap.json 2> gpurun_out/${TAG}_ab_overlap.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_overlap.log; [ $rc -eq 0 ] || exit $rc
+    STEPS=16 AB=CRDT_SORTED_FORM=0,8388608,6291456,14680064 timeout -k 10 300 python -u tools/prof_flags.py \
+      > gpurun_out/${TAG}_ab_flags.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_flags.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 12 --warmup 2 --ab CRDT_SORTED_FORM=0,8388608 --no-cpu \
+      --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_cfg3.json 2> gpurun_out/${TAG}_ab_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_cfg3.log; exit $rc ;;
+  flags)
+    # the flag passes' forms in one process (0: XCD order + 4-byte staging + 8-record gather; 2097152: plain order;
+    # 4194304: byte staging; 6291456: both old), under the kernel trace for the passes' own times
+    timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "flagged" > gpurun_out/${TAG}_pytest_flagged.log 2>&1 \
+      || { tail -40 gpurun_out/${TAG}_pytest_flagged.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_flagged.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_flags
+    STEPS=20 AB=CRDT_SORTED_FORM=0,2097152,4194304,6291456 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_flags -o run -- python3 tools/prof_flags.py \
+      > gpurun_out/${TAG}_ab_flags.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_flags.log; [ $rc -eq 0 ] || exit $rc
+    k=$(find gpurun_out/${TAG}_prof_flags -name "*kernel_stats.csv" | head -1)
+    grep -i "flags_back\|pflags\|scatter1\|scatter2_seg" "$k" | cut -c1-400 ;;
+  compact)
+    # the compact form: sorted parity subset (compact cases included), then in-process A/Bs on the fan-in and cfg3
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "sorted or compact or flagged_equals" \
+      > gpurun_out/${TAG}_pytest_sorted.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_sorted.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_sorted.log
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --ab CRDT_SORTED_FORM=0,1048576 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_compact.json 2> gpurun_out/${TAG}_ab_compact.log
+    rc=$?; grep "A/B\|placement" gpurun_out/${TAG}_ab_compact.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 12 --warmup 2 --ab CRDT_SORTED_FORM=0,1048576 --no-cpu \
+      --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_compact_cfg3.json 2> gpurun_out/${TAG}_ab_compact_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_compact_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 > gpurun_out/${TAG}_bench_default.json \
+      2> gpurun_out/${TAG}_bench_default.log
+    rc=$?; tail -2 gpurun_out/${TAG}_bench_default.log; exit $rc ;;
   full)
     timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/${TAG}_pytest_full.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_full.log; exit 1; }

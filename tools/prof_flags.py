@@ -21,6 +21,7 @@ t = DeviceTable(0, local_rank=0, capacity=wl["capacity"])
 t.set_rank_bound(1025)
 flags = torch.zeros(wl["total"], dtype=torch.uint8, device="cuda")
 times = {}
+ref = None                                # the first step's flags: every later step (any A/B value) must equal them
 for i in range(steps):
     if ab:
         os.environ[ab_var] = ab_vals[i % len(ab_vals)]
@@ -34,6 +35,12 @@ for i in range(steps):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - ts) * 1e3
     tag = os.environ.get(ab_var) if ab else ""
+    if fl is not False:
+        if ref is None:
+            ref = (flags.clone(), res["n_won"], res["canonical_lt"])
+        elif not (torch.equal(flags, ref[0]) and res["n_won"] == ref[1] and res["canonical_lt"] == ref[2]):
+            print(f"step {i} {tag}: FLAGS DIFFER from step 0", flush=True)
+            sys.exit(3)
     if i >= (len(ab_vals) if ab else 1):
         times.setdefault(tag, []).append(ms)
     print(f"step {i} {tag}: {ms:.2f} ms path {t.last_path()} flagged {t.last_plan()['flagged']} won {res['n_won']}",

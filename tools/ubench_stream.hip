@@ -53,6 +53,51 @@ __global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ a, u32x4
     }
 }
 
+// Block-contiguous copy (round 6): workgroup g copies the contiguous chunk [g * per, + per)
+// instead of striding over the grid — each workgroup streams one region of DRAM pages, as a partition tile does.
+template <int U>
+__global__ __launch_bounds__(256) void k_copy_blk(const u32x4* __restrict__ a, u32x4* __restrict__ b, uint64_t n,
+                                                  uint64_t per) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * per, c1 = c0 + per < n ? c0 + per : n;
+    for (uint64_t s = c0 + threadIdx.x; s < c1; s += 256 * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = s + (uint64_t)u * 256;
+            if (i < c1) v[u] = __builtin_nontemporal_load(a + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = s + (uint64_t)u * 256;
+            if (i < c1) b[i] = v[u];
+        }
+    }
+}
+
+// The level-1 scatter's shape without its ranking (round 6): a tile of T records (16 B each) read contiguously,
+// written as 256 runs of T / 256 records to 256 far-apart places — run d of tile t at d * (tiles * run) + t * run,
+// so the tiles' runs of one digit are adjacent, as in a partition.  Records of 16 B or (kNarrow) 12 + 2 B
+// (the 14-B level-1 record: payload column + key column).  XCD-contiguous tile order as in the library.
+template <int T, bool kNarrow>
+__global__ __launch_bounds__(1024) void k_scatter_runs(const u32x4* __restrict__ a, u32x4* __restrict__ b,
+                                                       uint32_t* __restrict__ b12, uint16_t* __restrict__ bk,
+                                                       uint32_t tiles, uint32_t per) {
+    const uint32_t t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (t >= tiles) return;
+    constexpr uint32_t run = T / 256;
+    for (uint32_t i = threadIdx.x; i < T; i += 1024) {
+        const u32x4 v = a[(uint64_t)t * T + i];
+        const uint32_t d = i / run, k = i % run;
+        const uint64_t o = (uint64_t)d * tiles * run + (uint64_t)t * run + k;
+        if (kNarrow) {
+            b12[3 * o] = v.x; b12[3 * o + 1] = v.y; b12[3 * o + 2] = v.z;
+            bk[o] = (uint16_t)v.w;
+        } else {
+            b[o] = v;
+        }
+    }
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ b, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
@@ -115,5 +160,41 @@ int main(int argc, char** argv) {
         WR(1) WR(4)
     }
     printf("BEST read %.0f GB/s, copy %.0f GB/s (r+w), write %.0f GB/s\n", best_r, best_c, best_w);
+    // round 6: block-contiguous copies, the runtime's device-to-device copy (what torch's copy_ and the bench's
+    // copy_GBs use), smaller buffers, and the level-1 scatter's own shape
+    double best_b = 0;
+    for (int wpc : {1, 2, 4}) {
+        const int grid = cus * wpc;
+        const uint64_t per = (n + grid - 1) / grid;
+#define CB(U) { float ms = best_ms([&] { k_copy_blk<U><<<grid, 256>>>(a, b, n, per); }); double r = 2 * gb / (ms * 1e-3); \
+                printf("copy-blk wg/CU %d U %d : %7.3f ms %7.0f GB/s (r+w)\n", wpc, U, ms, r); if (r > best_b) best_b = r; }
+        CB(4) CB(8)
+    }
+    {
+        float ms = best_ms([&] { CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0)); });
+        printf("hipMemcpy D2D : %7.3f ms %7.0f GB/s (r+w)\n", ms, 2 * gb / (ms * 1e-3));
+    }
+    for (uint64_t sub : {1ull << 30, 2ull << 30, 4ull << 30}) {
+        const uint64_t ns = sub / 16;
+        const int grid = cus * 2;
+        float ms = best_ms([&] { k_copy<8, true><<<grid, 256>>>(a, b, ns); });
+        printf("copy %4.1f GiB wg/CU 2 U 8 ntst : %7.3f ms %7.0f GB/s (r+w)\n", sub / double(1ull << 30), ms,
+               2 * (sub / 1e9) / (ms * 1e-3));
+    }
+    {
+        constexpr int T = 7168;                       // one level-1 sub-tile; runs of 28 records
+        const uint32_t tiles = (uint32_t)(n / T);
+        const uint32_t per = (tiles + 7) / 8;
+        const double recs = (double)tiles * T;
+        uint32_t* b12 = reinterpret_cast<uint32_t*>(b);
+        uint16_t* bk = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(b) + (uint64_t)(recs * 12) + 256);
+        float ms = best_ms([&] { k_scatter_runs<T, false><<<per * 8, 1024>>>(a, b, nullptr, nullptr, tiles, per); });
+        printf("scatter-runs 16B (256 runs of %d) : %7.3f ms %7.0f GB/s (r+w)\n", T / 256, ms, recs * 32 / 1e9 / (ms * 1e-3));
+        ms = best_ms([&] { k_scatter_runs<T, true><<<per * 8, 1024>>>(a, nullptr, b12, bk, tiles, per); });
+        printf("scatter-runs 12+2B (256 runs of %d) : %7.3f ms %7.0f GB/s (r+w)\n", T / 256, ms, recs * 30 / 1e9 / (ms * 1e-3));
+        const double seq = 2 * gb;
+        (void)seq;
+    }
+    printf("BEST copy-blk %.0f GB/s (r+w)\n", best_b);
     return 0;
 }
