@@ -921,7 +921,9 @@ def cpu_baseline_omp(wl, budget_s, table=None, keep=False):
     base = {"value": round(recs / el, 1), "unit": "records/s", "cores": threads, "kind": "port",
             "sample": f"first {done} of {wl['R']} changesets ({recs:,} records) merged by oracle/merge_omp.c "
                       f"(parallel per-changeset max / apply, exact recv loop only on flagged changesets), "
-                      f"{threads} OpenMP threads, {el:.1f}s"}
+                      f"{threads} OpenMP threads, {el:.1f}s",
+            "threads_why": "OMP_NUM_THREADS (16 on the GPU box: one GPU's share of its host; os.cpu_count() reports "
+                           "the whole machine, whose cores serve every GPU of the node), else min(cpu_count, 16)"}
     if keep:
         return base, parity, kept
     return base, parity

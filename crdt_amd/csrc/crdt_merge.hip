@@ -1149,7 +1149,8 @@ __global__ __launch_bounds__(256) void k_flags_back(const uint8_t* __restrict__ 
 
 // Part bookkeeping of a sharded merge: gsend[R + j] = records of this rank's part of j, and
 // gsend[2R .. 2R + 4) = this rank's record frame (Misc::fr_*, max-accumulators).
-constexpr uint32_t kGatherExtra = 6;     // the frame's 4 words, the rank's collective-shape word, its local status
+constexpr uint32_t kGatherExtra = 7;     // the frame's 4 words, the rank's collective-shape word, its local status,
+                                         // the records' largest lt & 0xFFFF (the compact frame, route_l1)
 // gsend[2R + 4] = cfg: the per-process settings that shape the collectives after the clock phase
 // (comm_path.inc, shard_cfg_word); k_shard_combine checks that every rank sent the same one.
 __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict__ offs, uint32_t R,
@@ -1165,6 +1166,7 @@ __global__ __launch_bounds__(256) void k_part_counts(const uint64_t* __restrict_
         gsend[2 * R + 3] = (long long)misc->fr_rhi;
         gsend[2 * R + 4] = cfg;
         gsend[2 * R + 5] = status;
+        gsend[2 * R + 6] = (long long)misc->fr_cmax;
     }
 }
 
@@ -1181,6 +1183,7 @@ __global__ __launch_bounds__(256) void k_fail_row(long long* __restrict__ gsend,
         for (int x = 0; x < 4; ++x) gsend[2 * R + x] = 0;
         gsend[2 * R + 4] = cfg;
         gsend[2 * R + 5] = status;
+        gsend[2 * R + 6] = 0;
     }
 }
 
@@ -1202,6 +1205,12 @@ __global__ __launch_bounds__(256) void k_shard_combine(const long long* __restri
             a = w[0] > a ? w[0] : a; b = w[1] > b ? w[1] : b; c = w[2] > c ? w[2] : c; d = w[3] > d ? w[3] : d;
         }
         misc->fr_lo = a; misc->fr_hi = b; misc->fr_rlo = (uint32_t)c; misc->fr_rhi = (uint32_t)d;
+        unsigned long long cm = 0;                          // the records' largest lt & 0xFFFF over the ranks
+        for (uint32_t r = 0; r < G; ++r) {
+            const unsigned long long x = (unsigned long long)g[r * row + 2ull * R + 6];
+            cm = x > cm ? x : cm;
+        }
+        misc->fr_cmax = cm;
         bool same = true;                                   // every rank's collective-shape word alike
         for (uint32_t r = 1; r < G; ++r) same = same && g[r * row + 2ull * R + 4] == g[2ull * R + 4];
         if (!same) misc->route_own = 4ull;                  // (k_route_plan has not run yet)
@@ -1675,6 +1684,7 @@ struct crdt_ctx {
                                     // 2: route_l1 always with the sender-side head fold; 3: folding every digit
     bool rl1_call_head = false;     // this call's route_l1 folds the owners' leading level-1 digits (the Zipf head)
     bool rl1_call_all = false;      // ... all of them (CRDT_ROUTE_L1=3: tests, A/B)
+    bool rl1_cmp = false;           // ... in the compact form (12-B level-1 records + 1-B digits; PackFrame::cb)
     bool last_rl1_head = false;     // ... the last routed merge's did
     uint64_t last_rl1_head_in = 0, last_rl1_head_out = 0;   // ... its head records before / after the fold
     uint32_t last_rl1_head_digits = 0;   // ... the leading level-1 digits it folded (Dh)

@@ -193,8 +193,12 @@ static int run(const Case* c, int mode) {
     } else if (mode == 5) {
         uint8_t id[CRDT_COMM_ID_BYTES];
         uint32_t nr = 0, rk = 9;
+        int32_t cst = -1;
+        const char* phase = NULL;
         if ((st = crdt_comm_unique_id(id)) != CRDT_OK || (st = crdt_comm_init_rccl(ctx, 1, 0, id)) != CRDT_OK ||
+            (st = crdt_set_comm_timeout(ctx, 300000)) != CRDT_OK ||     /* what GpuMapCrdt.sharded calls */
             (st = crdt_set_presharded(ctx, 1)) != CRDT_OK || (st = crdt_comm_info(ctx, &nr, &rk)) != CRDT_OK ||
+            (st = crdt_comm_state(ctx, &cst, &phase)) != CRDT_OK || cst != 0 || !phase ||
             nr != 1 || rk != 0) {
             fprintf(stderr, "mode 5 setup: %s\n", crdt_status_string(st));
             crdt_destroy(ctx);

@@ -57,6 +57,25 @@ case "${STAGE:-comm}" in
     timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 > gpurun_out/${TAG}_bench_default.json \
       2> gpurun_out/${TAG}_bench_default.log
     rc=$?; tail -2 gpurun_out/${TAG}_bench_default.log; exit $rc ;;
+  perf2)
+    # the flagged form's compact variant (parity subset, then the flagged merge with compact on / off in one process);
+    # the routed fan-in tests (head owner work beside the pieces) and the N = 8 loopback probe
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "flagged or compact or loopback or routed_fanin or eight_rank_route_l1" \
+      > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest.log
+    STEPS=12 AB=CRDT_SORTED_FORM=0,1048576 timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_ab_flags.log 2>&1
+    rc=$?; grep "A/B\|DIFFER\|step 0" gpurun_out/${TAG}_ab_flags.log; [ $rc -eq 0 ] || exit $rc
+    N=8 STEPS=3 MODES=route_l1,route_l1_head timeout -k 10 600 python -u tools/route_probe.py \
+      > gpurun_out/${TAG}_route_probe_n8.txt 2>&1
+    rc=$?; tail -25 gpurun_out/${TAG}_route_probe_n8.txt; exit $rc ;;
+  ceiling)
+    # the streaming ceilings the floors are priced at: the micro-benchmark (grid-stride and
+    # block-contiguous copies, the runtime's D2D copy, smaller buffers, the level-1 scatter's own shape), then the
+    # default bench line on the same box (its torch copy figure, gpu_clocks.copy_GBs)
+    timeout -k 10 300 ./tools/ubench_stream 8 > gpurun_out/${TAG}_ubench_stream.txt 2>&1
+    rc=$?; tail -12 gpurun_out/${TAG}_ubench_stream.txt; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 420 python -u bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
+    rc=$?; tail -2 gpurun_out/${TAG}_bench_default.log; exit $rc ;;
   full)
     timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/${TAG}_pytest_full.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_full.log; exit 1; }
