@@ -313,17 +313,23 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                     kk[kHist ? 4 * g : 0] = kv.x; kk[kHist ? 4 * g + 1 : 0] = kv.y;
                     kk[kHist ? 4 * g + 2 : 0] = kv.z; kk[kHist ? 4 * g + 3 : 0] = kv.w;
                 }
+                if (kEager) {     // (round 6: the ranks in 16-B loads too — the sharded scan's 4-B loads cost it)
+                    const u32x4u rv = *reinterpret_cast<const u32x4u*>(rank + i0);
+                    rk[kEager ? 4 * g : 0] = rv.x; rk[kEager ? 4 * g + 1 : 0] = rv.y;
+                    rk[kEager ? 4 * g + 2 : 0] = rv.z; rk[kEager ? 4 * g + 3 : 0] = rv.w;
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < kScanItems; ++q) {
             const uint64_t i = idx(q);
-            if (!kVec || !vec_done[kVec ? q >> 2 : 0]) {
+            const bool vd = kVec && vec_done[kVec ? q >> 2 : 0];
+            if (!vd) {
                 v[q] = i < end ? lt[i] : INT64_MIN;
                 if (kHist) kk[kHist ? q : 0] = i < end ? __builtin_nontemporal_load(sh.key + i) : UINT32_MAX;
             }
             if (kEager) {
-                rk[q] = i < end ? rank[i] : 0u;
+                if (!vd) rk[kEager ? q : 0] = i < end ? rank[i] : 0u;
                 if (kMillis) mv[kMillis ? q : 0] = (millis && i < end) ? millis[i] : 0;
             }
             m = imax(m, v[q]);

@@ -76,6 +76,12 @@ case "${STAGE:-comm}" in
     rc=$?; tail -12 gpurun_out/${TAG}_ubench_stream.txt; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 420 python -u bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
     rc=$?; tail -2 gpurun_out/${TAG}_bench_default.log; exit $rc ;;
+  profiles)
+    # the closing tree's evidence for the default command: the bench line under the kernel trace (bench.py's HIP-event
+    # average for the dominant kernel beside the trace's), then its HBM bytes (two --pmc passes) into PMC_OUT, which
+    # bench.py's roofline.traffic reads
+    TAG=$TAG bash tools/gpu_prof_same.sh || exit 1
+    PMC_OUT=${PMC_OUT:-r06_pmc_bench.json} bash tools/gpu_pmc_bench.sh ;;
   full)
     timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/${TAG}_pytest_full.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_full.log; exit 1; }
