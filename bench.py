@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 TIMING_EVERY = 8           # streaming configs (one merge call per delta): HIP-event timing sampled
-PMC_FILE = os.path.join(ROOT, "profiles", "r05b_pmc_bench.json")    # rocprofv3 --pmc of the default command
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_pmc_bench.json")    # rocprofv3 --pmc of the default command
 
 
 def log(*a):
