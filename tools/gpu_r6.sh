@@ -82,6 +82,24 @@ case "${STAGE:-comm}" in
     # bench.py's roofline.traffic reads
     TAG=$TAG bash tools/gpu_prof_same.sh || exit 1
     PMC_OUT=${PMC_OUT:-r06_pmc_bench.json} bash tools/gpu_pmc_bench.sh ;;
+  cfg3)
+    # cfg3 on the compact form: the level-1 tile and the sparse-bucket threshold re-tuned in one process each, then a
+    # kernel trace of five merges (per-kernel times against the floors)
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 12 --warmup 2 --ab CRDT_L1_TILE=0,28672 --no-cpu \
+      --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_cfg3_l1tile.json 2> gpurun_out/${TAG}_cfg3_l1tile.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_cfg3_l1tile.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 12 --warmup 2 --ab CRDT_SPARSE_T=2048,1024,4096 --no-cpu \
+      --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_cfg3_sparse.json 2> gpurun_out/${TAG}_cfg3_sparse.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_cfg3_sparse.log; [ $rc -eq 0 ] || exit $rc
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_cfg3
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg3 -o run \
+      -- python3 bench.py --config cfg3 --steps 5 --warmup 2 --no-cpu --no-pcie --no-census --flag-steps 0 \
+      > gpurun_out/${TAG}_prof_cfg3.json 2> gpurun_out/${TAG}_prof_cfg3.log
+    rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_cfg3.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt; head -16 gpurun_out/${TAG}_cfg3_full.txt
+    rm -f "$k" ;;
   full)
     timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/${TAG}_pytest_full.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_full.log; exit 1; }
