@@ -266,7 +266,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
     int64_t wall, uint32_t local_rank,
-    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh)
+    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh, bool jx = false)
 {
     // (kFrame without kEager: the lt frame only — the host declared a rank bound, crdt_set_rank_bound)
     __shared__ int64_t s_max[kScanThreads / 64];
@@ -274,12 +274,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
     __shared__ unsigned long long s_fr[kFrame ? 5 * (kScanThreads / 64) : 1];
     __shared__ uint32_t s_h[kHist ? 512 : 1];
     static_assert(!kHist || kScanThreads == 256, "one histogram bin per thread");
-    const uint32_t j = jbase + blockIdx.y;
+    // jx (the step-major grid): blockIdx.x is the changeset and blockIdx.y the step, so the workgroups run every
+    // changeset's first steps before any changeset's last (shorter) one — fewer, shorter tails when a batch is only
+    // a few workgroup rounds deep (cfg3: 4 steps of up to 7 tiles per changeset on ~1024 resident workgroups)
+    const uint32_t j = jbase + (jx ? blockIdx.x : blockIdx.y);
     const uint64_t beg = offs[j], end = offs[j + 1];
     const uint32_t t0 = tstart[j], nt = tstart[j + 1] - t0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr uint32_t kStep = kHist ? kHistSub : 1u;
-    for (uint32_t u = blockIdx.x; u * kStep < nt; u += gridDim.x) {
+    const uint32_t ustride = jx ? gridDim.y : gridDim.x;
+    for (uint32_t u = jx ? blockIdx.y : blockIdx.x; u * kStep < nt; u += ustride) {
       if (kHist) {
         s_h[threadIdx.x] = 0;
         s_h[256 + threadIdx.x] = 0;
@@ -1561,6 +1565,9 @@ constexpr uint32_t kFormNoOwnInPlace = 524288; // sharded merge: the own chunk c
 constexpr uint32_t kFormNoCompact = 1u << 20;   // no compact form (PackFrame::cb): 14-B / 13-B partition records
 constexpr uint32_t kFormFbackXcd = 1u << 21;
 constexpr uint32_t kFormFbackWide = 1u << 22;
+constexpr uint32_t kFormScanJx = 1u << 24;      // the clock scan's step-major grid (k_scan's jx) on every batch
+constexpr uint32_t kFormNoScanJx = 1u << 25;    // ... on none (default: batches of at most kScanJxMax workgroups)
+constexpr uint32_t kScanJxMax = 8192;           // ~8 rounds of the ~1024 resident scan workgroups (cfg3: 4096)
 constexpr uint32_t kFormOverlap = 1u << 23;      // sorted path: split buckets' fold / carry beside the unsplit
                                                  // buckets' resolve (measured slower: opt-in)
 constexpr uint32_t kPartPad = 1024;          // records of slack behind every partition buffer (tile-end vector loads)
@@ -2035,45 +2042,52 @@ int phase_scan(crdt_ctx* c, const crdt_batch* home, int64_t wall, long long* d_m
         const uint32_t cap_x = std::max<uint32_t>(1, 65536u / std::max<uint32_t>(R, 1));
         const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(mt, cap_x));
         const uint32_t gxh = std::max<uint32_t>(1, std::min<uint32_t>((mt + kHistSub - 1) / kHistSub, cap_x));
+        // step-major grid where the batch is only a few workgroup rounds deep (the rounds' tail is what it
+        // shortens: cfg3 0.337 -> 0.303 ms); changeset-major otherwise (the 1B fan-in's 35 rounds: a tie)
+        const bool hgrid = hist || rhist;
+        const uint64_t nwg = (uint64_t)(hgrid ? gxh : gx) * R;
+        const bool jx = !(c->form_off & kFormNoScanJx) && ((c->form_off & kFormScanJx) || nwg <= kScanJxMax);
         for (uint32_t jb = 0; jb < R; jb += 65535) {
             const uint32_t gy = std::min<uint32_t>(65535, R - jb);
+            const dim3 gdh = jx ? dim3(gy, std::min<uint32_t>(gxh, 65535)) : dim3(gxh, gy);
+            const dim3 gd = jx ? dim3(gy, std::min<uint32_t>(gx, 65535)) : dim3(gx, gy);
             if (rhist)                                    // routed histogram: rank read with lt (the frame)
-                k_scan<true, false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<true, false, true, true, true><<<gdh, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shr);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shr, jx);
             else if (hist && !(c->form_off & kFormNoVecScan))
-                k_scan<false, true, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<false, true, true, true, true><<<gdh, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
                     c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p,
-                    shist);
+                    shist, jx);
             else if (hist)
-                k_scan<false, true, true, true><<<dim3(gxh, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<false, true, true, true><<<gdh, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shist);
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, shist, jx);
             else if (c->frame_lt_only)                    // lt frame only: ranks loaded lazily as usual
-                k_scan<false, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<false, true, true><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
             else if (frame && !cols.millis)
-                k_scan<true, false, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<true, false, true><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
             else if (frame)
-                k_scan<true, true, true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<true, true, true><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
             else if (c->scan_eager && !cols.millis)
-                k_scan<true, false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<true, false><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, nullptr, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
             else if (c->scan_eager)
-                k_scan<true><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<true><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
             else
-                k_scan<false><<<dim3(gx, gy), kScanThreads, 0, c->stream>>>(
+                k_scan<false><<<gd, kScanThreads, 0, c->stream>>>(
                     cols.lt, cols.rank, cols.millis, c->d_offs, c->d_tstart, jb, c->canonical, wall,
-                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{});
+                    c->local_rank, c->d_T.p, c->d_misc, c->d_candtile.p, ScanHist{}, jx);
         }
         if (!c->fused)
             k_tmax<<<std::min<uint32_t>(R, 4096), 256, 0, c->stream>>>(c->d_T.p, c->d_tstart, R, d_maxima);

@@ -1099,7 +1099,7 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
 
 
 @pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536",
-                                      "8388608"])
+                                      "8388608", "16777216", "33554432"])
 def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
@@ -1110,8 +1110,25 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False, capacity=(1 << 20) + 3,
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
-    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536", "8388608")), \
+    assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536", "8388608",
+                                                 "16777216", "33554432")), \
         res["plan"]
+
+
+@pytest.mark.parametrize("grid", ["16777216", "33554432"])
+@pytest.mark.parametrize("k", range(4))
+@pytest.mark.parametrize("path", ["gather", "sorted"])
+def test_scan_step_major_grid(gpu_device, monkeypatch, k, path, grid):
+    """CRDT_SORTED_FORM bits 16777216 / 33554432: the clock scan's step-major grid (changeset in blockIdx.x,
+    step in blockIdx.y) forced on / off (by default it runs on batches of at most 8192 scan workgroups) —
+    the same tile maxima, raising tiles and fused level-1 histogram, so the same rows and exception fields
+    as the oracle, on multi-step changesets with a forced drift / duplicate-node record."""
+    monkeypatch.setenv("CRDT_SORTED_FORM", grid)
+    case = list(_fused_cases())[k]
+    kw = dict(path=path)
+    if path == "sorted":
+        kw.update(flags=False, counts=False, rank_bound=int(case["rank"].max()) + 1, device_cols=True)
+    compare_with_oracle(case, **kw)
 
 
 @pytest.mark.parametrize("sparse_t", ["0", "1024", "1000000000"])

@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT=${OUT:-pmc_flags_sq}
 rm -rf gpurun_out/$OUT
-MIX=1 STEPS=4 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d gpurun_out/$OUT -o run -- python3 tools/prof_flags.py > gpurun_out/$OUT.log 2>&1
+CTRS=${CTRS:-SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU}
+MIX=1 STEPS=4 timeout -s KILL 240 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/$OUT -o run -- python3 tools/prof_flags.py > gpurun_out/$OUT.log 2>&1
 rc=$?; echo "[pmc] exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/$OUT.log; exit $rc; }
 OUT=$OUT python3 - <<'PY'
 import csv, glob, collections, os
@@ -22,7 +23,7 @@ for r in csv.DictReader(open(f)):
 for k, c in acc.items():
     if c.get("SQ_WAVE_CYCLES", 0) < 1e8: continue
     w = c["SQ_WAVE_CYCLES"]
-    print(f"{k[:60]:60s} waitany {c['SQ_WAIT_ANY']/w:.2f} waitlds {c['SQ_WAIT_INST_LDS']/w:.2f} "
-          f"ldsconf/ldsinst {c['SQ_LDS_BANK_CONFLICT']/max(c['SQ_INSTS_LDS'],1):.2f} "
-          f"lds/valu {c['SQ_INSTS_LDS']/max(c['SQ_INSTS_VALU'],1):.2f} valu {c['SQ_INSTS_VALU']:.3g} lds {c['SQ_INSTS_LDS']:.3g}")
+    print(f"{k[:60]:60s} " + "  ".join(
+        f"{n[3:]} {v / w:.3f}" if n.startswith(("SQ_WAIT", "SQ_ACTIVE", "SQ_BUSY")) else f"{n[3:]} {v:.4g}"
+        for n, v in sorted(c.items())))
 PY

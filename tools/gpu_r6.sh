@@ -100,6 +100,39 @@ case "${STAGE:-comm}" in
     k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
     python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt; head -16 gpurun_out/${TAG}_cfg3_full.txt
     rm -f "$k" ;;
+  scanjx)
+    # the clock scan's step-major grid (CRDT_SORTED_FORM bit 16777216): parity subset, then in-process A/Bs on cfg3
+    # (four steps per changeset: the workgroup rounds' tail) and the 1B fan-in
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "scan_step_major or packed_form_switches or fused_small" \
+      > gpurun_out/${TAG}_pytest_scanjx.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_scanjx.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_scanjx.log
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,16777216 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanjx_cfg3.json 2> gpurun_out/${TAG}_ab_scanjx_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanjx_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,16777216 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanjx.json 2> gpurun_out/${TAG}_ab_scanjx.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanjx.log; exit $rc ;;
+  cfg3b)
+    # the scan grid's default (auto: step-major on cfg3) against forced changeset-major, parity subset first; then the
+    # flag passes' SQ counters (stage flagsq)
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "scan_step_major or packed_form_switches or fused_small" \
+      > gpurun_out/${TAG}_pytest_scanjx.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_scanjx.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_scanjx.log
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,33554432 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanjx_cfg3.json 2> gpurun_out/${TAG}_ab_scanjx_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanjx_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    STAGE=flagsq TAG=$TAG bash tools/gpu_r6.sh ;;
+  flagsq)
+    # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
+    # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
+    export TMPDIR=/tmp
+    timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1 || exit 1
+    C2="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU"
+    for c in $C2; do grep -qw "$c" gpurun_out/${TAG}_counters.txt || { echo "no counter $c"; exit 1; }; done
+    OUT=${TAG}_pmc_flags_sq bash tools/gpu_pmc_flags.sh > gpurun_out/${TAG}_pmc_flags_sq.txt 2>&1
+    rc=$?; cat gpurun_out/${TAG}_pmc_flags_sq.txt | cut -c1-400; [ $rc -eq 0 ] || exit $rc
+    CTRS="$C2" OUT=${TAG}_pmc_flags_sq2 bash tools/gpu_pmc_flags.sh > gpurun_out/${TAG}_pmc_flags_sq2.txt 2>&1
+    rc=$?; cat gpurun_out/${TAG}_pmc_flags_sq2.txt | cut -c1-400; exit $rc ;;
   full)
     timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/${TAG}_pytest_full.log 2>&1 \
       || { tail -40 gpurun_out/${TAG}_pytest_full.log; exit 1; }
