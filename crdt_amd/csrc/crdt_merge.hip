@@ -1567,6 +1567,10 @@ constexpr uint32_t kFormFbackXcd = 1u << 21;
 constexpr uint32_t kFormFbackWide = 1u << 22;
 constexpr uint32_t kFormScanJx = 1u << 24;      // the clock scan's step-major grid (k_scan's jx) on every batch
 constexpr uint32_t kFormNoScanJx = 1u << 25;    // ... on none (default: batches of at most kScanJxMax workgroups)
+constexpr uint32_t kFormNoItemLists = 1u << 28; // the order-free packed resolve's kernels over every item slot
+constexpr uint32_t kFormNoFbackPre = 1u << 27;  // the flag passes of round 5 (k_flags_back), not k_flags_back_pre
+constexpr uint32_t kFormFbackPre512 = 1u << 29; // k_flags_back_pre's level-2 pass in 512-thread workgroups (not 256)
+constexpr uint32_t kFormNoSparseK = 1u << 26;   // sparse buckets inside k_resolve_packed (not k_resolve_sparse)
 constexpr uint32_t kScanJxMax = 8192;           // ~8 rounds of the ~1024 resident scan workgroups (cfg3: 4096)
 constexpr uint32_t kFormOverlap = 1u << 23;      // sorted path: split buckets' fold / carry beside the unsplit
                                                  // buckets' resolve (measured slower: opt-in)
@@ -1650,6 +1654,8 @@ struct crdt_ctx {
     DBuf<uint32_t> p_hist, p_toff, p_part, p_choff, p_dstart1, p_dstart2, p_l2map;
     DBuf<uint64_t> p_plan, p_l1beg;
     DBuf<uint32_t> p_ibase, p_ksu32, p_tseg, p_ibucket;   // resolve items per bucket; part-state / carry u32 columns
+    DBuf<uint32_t> p_ilist;                  // k_item_lists: per-kernel item lists of the order-free packed resolve
+    HBuf<uint32_t> h_ilist;                  // (pinned) their counts
     DBuf<int64_t> p_kslt;
     HBuf<uint64_t> h_pplan;
     bool last_sorted = false;       // the last crdt_merge ran the sorted path
@@ -2470,7 +2476,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     if (fl) {
         uint64_t ncol = 0;                                           // input index space of pos1
         for (size_t s = 0; s < ns_all; ++s) ncol = std::max<uint64_t>(ncol, sg.end[s]);
-        HIPALLOC(c->f_pos1.ensure(ncol ? ncol : 1));
+        HIPALLOC(c->f_pos1.ensure((ncol ? ncol : 1) + 8));   // + 8: k_flags_back_pre's clamped loads
     }
     for (size_t sb = 0; sb < ns_all;) {
         // window [jb, jb + win): kWindow changesets (the kj word's field), the packed key's W
@@ -2690,7 +2696,7 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const uint32_t nt2s = (uint32_t)((nw + ts2 - 1) / ts2) + kDigits;
             const uint32_t xper2 = c->xcd_map ? (nt2s + kXcds - 1) / kXcds : 0;
             if (ord) {         // changeset order kept in every final bucket; level-2 run offsets kept
-                if (fl) HIPALLOC(c->f_pos2.ensure(nw));
+                if (fl) HIPALLOC(c->f_pos2.ensure(nw + 8));
                 uint16_t* pos2 = fl ? c->f_pos2.p : nullptr;
                 const Rec12* i12 = reinterpret_cast<const Rec12*>(p1r);
                 Rec12* o12 = reinterpret_cast<Rec12*>(p2r);
@@ -2754,6 +2760,22 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                                                                     em ? c->e_bbase.p : nullptr);
         k_seg_index<<<std::min<uint32_t>(grid_for(max_items, 256), 4096), 256, 0, c->stream>>>(d_ib, nb, max_items,
                                                                                                c->p_ibucket.p);
+        // k_item_lists, then the host's wait for its counts (the packed resolve's kernels on exactly their items)
+        auto item_lists = [&](uint64_t hw_s, uint32_t sparse_s, uint32_t* n_fold, uint32_t* n_dense, uint32_t* n_sparse,
+                              uint32_t* n_hot, uint32_t* n_items) -> int {
+            HIPALLOC(c->p_ilist.ensure(kListHead + 3 * (size_t)max_items));
+            HIPALLOC(c->h_ilist.ensure(kListHead));
+            k_item_lists<<<(nb + 1023) / 1024, 1024, 0, c->stream>>>(bst, nb, d_ib, d_hb, d_hot, hw_s, sparse_s,
+                                                                    c->p_ilist.p, max_items);
+            HIPCHK(hipMemcpyAsync(c->h_ilist.p, c->p_ilist.p, kListHead * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            const uint32_t* h = c->h_ilist.p;
+            if (h[0] > max_items || h[1] > max_items || h[2] > max_items || h[3] > max_hot || h[4] > max_items)
+                return CRDT_E_HIP;                              // (cannot happen: the lists hold <= max_items)
+            *n_fold = h[0]; *n_dense = h[1]; *n_sparse = h[2]; *n_hot = h[3]; *n_items = h[4];
+            return CRDT_OK;
+        };
         if (em) {          // map-side combine: part folds, then every key's maximum emitted
             // emit items: the resolve's max_items, then 16 carry blocks per hot bucket; the slots are the
             // buckets' (k_bucket_items' ebase: min(kSKeys, records) each), so at most min(records, key range)
@@ -2804,37 +2826,47 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             uint8_t* fl2 = fl ? c->f_flag2.p : nullptr;
             // the split buckets' part folds and carry-ins on the side stream, beside the unsplit buckets' ordered
             // resolve (disjoint buckets: their rows, states and flags do not meet); then the split buckets' walk
-            int st = ov ? overlap_fork(c) : CRDT_OK;
-            if (st) return st;
+            // the fold and the carry-ins on exactly their items (k_item_lists), the walk on the items there are
+            int st = CRDT_OK;
+            uint32_t g_fold = max_items, g_hot = max_hot, g_items = max_items, g_d, g_s;
+            const uint32_t* l_fold = nullptr;
+            if (!c->has_comm && !(c->form_off & kFormNoItemLists)) {
+                if ((st = item_lists(0, 0, &g_fold, &g_d, &g_s, &g_hot, &g_items))) return st;
+                l_fold = c->p_ilist.p + kListHead;
+            }
+            if ((st = ov ? overlap_fork(c) : CRDT_OK)) return st;
             const hipStream_t fs = ov ? c->sstream : c->stream;
-            if (cmp)
-                k_resolve_packed<true, true, false, false, true><<<max_items, kQThreads, 0, fs>>>(
+            if (!g_fold) {
+            } else if (cmp)
+                k_resolve_packed<true, true, false, false, true><<<g_fold, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
-                    ps_key, ps_val, pf, c->d_misc);
+                    ps_key, ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
             else if (k8)
-                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
+                k_resolve_packed<true, true, true><<<g_fold, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
-                    ps_val, pf, c->d_misc);
+                    ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
             else
-                k_resolve_packed<true><<<max_items, kQThreads, 0, fs>>>(
+                k_resolve_packed<true><<<g_fold, kQThreads, 0, fs>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
-                    ps_val, pf, c->d_misc);
-            k_part_cin_packed<<<dim3(kSKeys / 256, max_hot), 256, 0, fs>>>(
-                d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
-                reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
+                    ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
+            if (g_hot)
+                k_part_cin_packed<<<dim3(kSKeys / 256, g_hot), 256, 0, fs>>>(
+                    d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, pf, c->d_misc,
+                    reinterpret_cast<uint64_t*>(c->f_cin_key.p), c->f_cin_val.p, c->f_cin_pres.p);
             const uint64_t* cink = reinterpret_cast<const uint64_t*>(c->f_cin_key.p);
             for (uint32_t which = ov ? 1u : 0u; which <= (ov ? 2u : 0u); ++which) {
                 if (which == 2 && (st = overlap_join(c))) return st;
-                if (cmp)
-                    k_resolve_pflags<false, true><<<max_items, kRThreads, 0, c->stream>>>(
+                if (!g_items) {
+                } else if (cmp)
+                    k_resolve_pflags<false, true><<<g_items, kRThreads, 0, c->stream>>>(
                         bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p,
                         jb, cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
                 else if (k8)
-                    k_resolve_pflags<true><<<max_items, kRThreads, 0, c->stream>>>(
+                    k_resolve_pflags<true><<<g_items, kRThreads, 0, c->stream>>>(
                         bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
                         cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
                 else
-                    k_resolve_pflags<false><<<max_items, kRThreads, 0, c->stream>>>(
+                    k_resolve_pflags<false><<<g_items, kRThreads, 0, c->stream>>>(
                         bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
                         cink, c->f_cin_val.p, c->f_cin_pres.p, pf, c->d_misc, fl2, which);
             }
@@ -2851,7 +2883,15 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     else                                                                                                  \
         k_flags_back<false, CHK, kPTile, W><<<xcd_grid(nt2f, fx), 512, 0, c->stream>>>(                   \
             tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc, xf2)
-                if (c->form_off & kFormFbackWide) { CRDT_FBACK2(6, true); }
+                const bool pre2 = !(c->form_off & (kFormNoFbackPre | kFormFbackWide)) && !fx &&
+                                  tm2f.tsize == (uint32_t)kPTile2;
+                if (pre2 && (c->form_off & kFormFbackPre512))
+                    k_flags_back_pre<false, 6, kPTile2, 16><<<nt2f, 512, 0, c->stream>>>(
+                        tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc);
+                else if (pre2)
+                    k_flags_back_pre<false, 6, kPTile2, 32, 256><<<nt2f, 256, 0, c->stream>>>(
+                        tm2f, h2f, t2f, c->f_pos2.p, c->f_flag2.p, c->f_flag1.p, c->d_misc);
+                else if (c->form_off & kFormFbackWide) { CRDT_FBACK2(6, true); }
                 else if (c->fback_chk == 4) { CRDT_FBACK2(4, false); }
                 else if (c->fback_chk == 6) { CRDT_FBACK2(6, false); }
                 else { CRDT_FBACK2(0, false); }
@@ -2867,7 +2907,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     k_flags_back<true, CHK, kPTile, W><<<xcd_grid(nt1, fx1), 512, 0, c->stream>>>(                        \
         tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc, xf1)
             if (fl) {
-                if (c->form_off & kFormFbackWide) { CRDT_FBACK1(6, true); }
+                if (!(c->form_off & (kFormNoFbackPre | kFormFbackWide)) && !fx1)
+                    k_flags_back_pre<true, 6, kPTile, 14><<<nt1, 512, 0, c->stream>>>(
+                        tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc);
+                else if (c->form_off & kFormFbackWide) { CRDT_FBACK1(6, true); }
                 else if (c->fback_chk == 4) { CRDT_FBACK1(4, false); }
                 else if (c->fback_chk == 6) { CRDT_FBACK1(6, false); }
                 else { CRDT_FBACK1(0, false); }
@@ -2886,27 +2929,47 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
             const Rec12* rec12 = reinterpret_cast<const Rec12*>(rec);
             // the split buckets' part folds + carry (they write the split buckets' rows) on the side stream, beside
             // the unsplit buckets' resolve (the other rows): disjoint buckets, joined before the next window
-            int st = ov ? overlap_fork(c) : CRDT_OK;
-            if (st) return st;
+            // the sparse buckets in k_resolve_sparse's small workgroups (the dense ones skip them)
+            const bool spk = c->sparse_t > 0 && !(c->form_off & (kFormNoSparseK | kFormNoWholeLines));
+            // each kernel on exactly its items (k_item_lists; the host waits for the four counts — by then the GPU is
+            // at the resolve, and the launches below follow at once)
+            int st = CRDT_OK;
+            const bool lists = !c->has_comm && !(c->form_off & (kFormNoItemLists | kFormNoWholeLines));
+            uint32_t g_fold = max_items, g_dense = max_items, g_sparse = max_items, g_hot = max_hot;
+            const uint32_t *l_fold = nullptr, *l_dense = nullptr, *l_sparse = nullptr;
+            if (lists) {
+                uint32_t g_items;
+                if ((st = item_lists(spk ? c->hw_read : 0, spk ? c->sparse_t : 0, &g_fold, &g_dense, &g_sparse, &g_hot,
+                                     &g_items)))
+                    return st;
+                l_fold = c->p_ilist.p + kListHead;
+                l_dense = l_fold + max_items;
+                l_sparse = l_dense + max_items;
+            }
+            if ((st = ov ? overlap_fork(c) : CRDT_OK)) return st;
             const hipStream_t fs = ov ? c->sstream : c->stream;
-            if (cmp)
-                k_resolve_packed<true, true, false, false, true><<<max_items, kQThreads, 0, fs>>>(
+            if (g_fold) {
+                if (cmp)
+                    k_resolve_packed<true, true, false, false, true><<<g_fold, kQThreads, 0, fs>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
+                        ps_key, ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
+                else if (k8)
+                    k_resolve_packed<true, true, true><<<g_fold, kQThreads, 0, fs>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
+                        ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
+                else
+                    k_resolve_packed<true><<<g_fold, kQThreads, 0, fs>>>(
+                        bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key,
+                        ps_val, pf, c->d_misc, EmitOut{}, 0, false, l_fold);
+            }
+            if (g_hot)
+                k_part_carry_packed<false><<<dim3(kSKeys / 256, g_hot), 256, 0, fs>>>(
+                    d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
+            if (!g_dense) {
+            } else if (cmp)
+                k_resolve_packed<false, true, false, false, true><<<g_dense, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
-                    ps_key, ps_val, pf, c->d_misc);
-            else if (k8)
-                k_resolve_packed<true, true, true><<<max_items, kQThreads, 0, fs>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc);
-            else
-                k_resolve_packed<true><<<max_items, kQThreads, 0, fs>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc);
-            k_part_carry_packed<false><<<dim3(kSKeys / 256, max_hot), 256, 0, fs>>>(
-                d_hot, d_ib, d_hb, c->table, c->cap, c->hw_read, ps_key, ps_val, c->d_Rj.p, jb, pf, c->d_misc);
-            if (cmp)
-                k_resolve_packed<false, true, false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
-                    bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->cap, c->hw_read, c->d_Rj.p, jb,
-                    ps_key, ps_val, pf, c->d_misc, EmitOut{}, c->sparse_t);
+                    ps_key, ps_val, pf, c->d_misc, EmitOut{}, c->sparse_t, spk, l_dense);
             else if ((c->form_off & kFormNoWholeLines) && k8)      // (13-B records: 1-B key column)
                 k_resolve_packed<false, false, true><<<max_items, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
@@ -2916,13 +2979,26 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
                     pf, c->d_misc);
             else if (k8)
-                k_resolve_packed<false, true, true><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<false, true, true><<<g_dense, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, EmitOut{}, c->sparse_t);
+                    pf, c->d_misc, EmitOut{}, c->sparse_t, spk, l_dense);
             else
-                k_resolve_packed<false><<<max_items, kQThreads, 0, c->stream>>>(
+                k_resolve_packed<false><<<g_dense, kQThreads, 0, c->stream>>>(
                     bst, d_ib, d_hb, c->p_ibucket.p, nb, rec12, rv, c->table, c->cap, c->hw_read, c->d_Rj.p, jb, ps_key, ps_val,
-                    pf, c->d_misc, EmitOut{}, c->sparse_t);
+                    pf, c->d_misc, EmitOut{}, c->sparse_t, spk, l_dense);
+            if (!spk || !g_sparse) {
+            } else if (cmp)
+                k_resolve_sparse<false, true><<<g_sparse, kSpThreads, 0, c->stream>>>(
+                    bst, d_ib, c->p_ibucket.p, nb, rec12, nullptr, c->table, c->hw_read, c->d_Rj.p, jb, pf, c->d_misc,
+                    c->sparse_t, l_sparse);
+            else if (k8)
+                k_resolve_sparse<true, false><<<g_sparse, kSpThreads, 0, c->stream>>>(
+                    bst, d_ib, c->p_ibucket.p, nb, rec12, rv, c->table, c->hw_read, c->d_Rj.p, jb, pf, c->d_misc,
+                    c->sparse_t, l_sparse);
+            else
+                k_resolve_sparse<false, false><<<g_sparse, kSpThreads, 0, c->stream>>>(
+                    bst, d_ib, c->p_ibucket.p, nb, rec12, rv, c->table, c->hw_read, c->d_Rj.p, jb, pf, c->d_misc,
+                    c->sparse_t, l_sparse);
             if (ov && (st = overlap_join(c))) return st;
         } else {           // order-free list form; split buckets finished by k_part_carry<true>
             k_resolve<true, true><<<max_items, kRThreads, 0, c->stream>>>(bst, d_ib, d_hb, c->p_ibucket.p, nb, rec,
@@ -3224,7 +3300,7 @@ void crdt_destroy(crdt_ctx* c) {
     c->p_dstart1.release(); c->p_dstart2.release(); c->p_l2map.release();
     c->p_plan.release(); c->p_l1beg.release(); c->h_pplan.release();
     c->p_ibase.release(); c->p_ksu32.release(); c->p_kslt.release(); c->p_tseg.release();
-    c->p_ibucket.release();
+    c->p_ibucket.release(); c->p_ilist.release(); c->h_ilist.release();
     c->f_pos1.release(); c->f_pos2.release(); c->f_flag1.release(); c->f_flag2.release();
     c->f_cin_key.release(); c->f_cin_val.release(); c->f_cin_pres.release();
     c->f_hist2.release(); c->f_toff2.release();

@@ -1099,7 +1099,7 @@ def test_rank_bound_violation_stores_nothing(gpu_device, counts):
 
 
 @pytest.mark.parametrize("form_off", ["64", "128", "256", "448", "512", "1024", "8192", "32768", "65536",
-                                      "8388608", "16777216", "33554432"])
+                                      "8388608", "16777216", "33554432", "67108864", "268435456"])
 def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
     """CRDT_SORTED_FORM: each refinement of the packed form switched off (changed-rows-only
     resolve writes, 16-B final records, 16-B level-1 records, forward-only tile fill, the
@@ -1111,7 +1111,7 @@ def test_sorted_packed_form_switches(gpu_device, monkeypatch, form_off):
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
     assert res["plan"]["key8"] == (form_off in ("64", "256", "512", "1024", "8192", "32768", "65536", "8388608",
-                                                 "16777216", "33554432")), \
+                                                 "16777216", "33554432", "67108864", "268435456")), \
         res["plan"]
 
 
@@ -1131,20 +1131,38 @@ def test_scan_step_major_grid(gpu_device, monkeypatch, k, path, grid):
     compare_with_oracle(case, **kw)
 
 
+@pytest.mark.parametrize("form", ["0", "1048576", "67108864"])
 @pytest.mark.parametrize("sparse_t", ["0", "1024", "1000000000"])
 @pytest.mark.parametrize("seed", [99, 5])
-def test_sorted_sparse_bucket_resolve(gpu_device, monkeypatch, sparse_t, seed):
+def test_sorted_sparse_bucket_resolve(gpu_device, monkeypatch, sparse_t, seed, form):
     """CRDT_SPARSE_T: buckets of fewer records than it fold their records from "absent" and read only
     the touched keys' rows afterwards (0: every bucket loads its rows first; 10^9: every bucket below
     the high-water mark is sparse) — the same rows, canonical and exception fields as the oracle, on
     frame edges (rows below / at / above the frame, ranks outside it, exact ties) and on a case where a
-    part of the table lies above the high-water mark."""
+    part of the table lies above the high-water mark.  Each in k_resolve_sparse's own workgroups (the
+    default; 1048576: on the 13-B records of the plain lt field) and inside k_resolve_packed (67108864)."""
     monkeypatch.setenv("CRDT_SPARSE_T", sparse_t)
+    monkeypatch.setenv("CRDT_SORTED_FORM", form)
     case = _frame_edge_case(seed) if seed == 99 else _cold_bucket_case(seed)
     res = compare_with_oracle(case, path="sorted", flags=False, counts=False,
                               capacity=(1 << 20) + 3 if seed == 99 else case["n_ids"],
                               rank_bound=int(case["rank"].max()) + 1, device_cols=True)
     assert res["plan"]["packed"] and res["plan"]["two_level"]
+
+
+@pytest.mark.parametrize("form", ["0", "1048576", "128"])
+def test_sorted_sparse_kernel_many_rounds(gpu_device, monkeypatch, form):
+    """k_resolve_sparse over buckets of 32768 records (CRDT_SPARSE_T = 10^9: every unsplit bucket is
+    sparse): 16 rounds of 2048 records each, the second phase re-reading them; ties across changesets
+    (few millis, small counters), tombstones and invisible rows — the oracle's rows and fields, on the
+    compact, 13-B (1048576) and 16-B (128) record forms."""
+    monkeypatch.setenv("CRDT_SPARSE_T", "1000000000")
+    monkeypatch.setenv("CRDT_SORTED_FORM", form)
+    case = make_case(seed=4242, n_local=10000, n_new=6384, R=8, per_cs=16384, millis_span=3, counter_span=3,
+                     n_ranks=5, neg_mod_frac=0.05, local_rank=1)
+    res = compare_with_oracle(case, path="sorted", flags=False, counts=False,
+                              rank_bound=int(case["rank"].max()) + 1, device_cols=True)
+    assert res["plan"]["packed"]
 
 
 def _cold_bucket_case(seed):
@@ -1802,14 +1820,17 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
     assert res["path"] == "gather" and not res["plan"]["flagged"]
 
 
-@pytest.mark.parametrize("chk,form", [("0", "0"), ("4", "0"), ("6", "0"), ("6", "4194304"), ("6", "2097152"),
-                                      ("6", "8388608"), ("6", "14680064")])
+@pytest.mark.parametrize("chk,form", [("0", "134217728"), ("4", "134217728"), ("6", "134217728"), ("6", "0"),
+                                      ("6", "4194304"), ("6", "2097152"), ("6", "8388608"), ("6", "14680064"),
+                                      ("6", "536870912"), ("6", "268435456")])
 def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, form):
-    """The flag passes: the one-byte staging with its run search without checkpoints (CRDT_FBACK_CHK=0), one
-    per 16 staged bytes (4) and one per 64 (6, the default); the opt-in forms of CRDT_SORTED_FORM: four-byte
+    """The flag passes: round 5's one-byte staging (CRDT_SORTED_FORM bit 134217728) with its run search without
+    checkpoints (CRDT_FBACK_CHK=0), one per 16 staged bytes (4) and one per 64 (6); the default k_flags_back_pre
+    (positions loaded first, one checkpoint per 64 staged bytes); the opt-in forms of CRDT_SORTED_FORM: four-byte
     staging with eight-record gathers (4194304), the scatters' XCD tile order (2097152), the split buckets' fold
-    and carry-ins on a side stream beside the unsplit buckets' walk (8388608), all three (14680064): split hot
-    bucket, cold buckets on the 2-B level-1 key column, a late drift — same flags, rows and counts as the
+    and carry-ins on a side stream beside the unsplit buckets' walk (8388608), all three (14680064);
+    k_flags_back_pre's level-2 pass in 512-thread workgroups (536870912); the fold and walk over every item slot
+    (268435456): split hot bucket, cold buckets on the 2-B level-1 key column, a late drift — same flags, rows and counts as the
     oracle."""
     monkeypatch.setenv("CRDT_FBACK_CHK", chk)
     monkeypatch.setenv("CRDT_SORTED_FORM", form)

@@ -122,6 +122,82 @@ case "${STAGE:-comm}" in
       --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanjx_cfg3.json 2> gpurun_out/${TAG}_ab_scanjx_cfg3.log
     rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanjx_cfg3.log; [ $rc -eq 0 ] || exit $rc
     STAGE=flagsq TAG=$TAG bash tools/gpu_r6.sh ;;
+  sparsek)
+    # the sparse buckets in their own kernel (k_resolve_sparse; CRDT_SORTED_FORM bit 67108864 = inside k_resolve_packed):
+    # parity subset, in-process A/B on cfg3 and the fan-in, then cfg3's kernel trace
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "sparse or packed_form_switches or sorted_compact or scan_step_major" \
+      > gpurun_out/${TAG}_pytest_sparsek.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_sparsek.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_sparsek.log
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,67108864 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_sparsek_cfg3.json 2> gpurun_out/${TAG}_ab_sparsek_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_sparsek_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,67108864 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_sparsek.json 2> gpurun_out/${TAG}_ab_sparsek.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_sparsek.log; [ $rc -eq 0 ] || exit $rc
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_cfg3
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg3 -o run \
+      -- python3 bench.py --config cfg3 --steps 5 --warmup 2 --no-cpu --no-pcie --no-census --flag-steps 0 \
+      > gpurun_out/${TAG}_prof_cfg3.json 2> gpurun_out/${TAG}_prof_cfg3.log
+    rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_cfg3.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt; head -24 gpurun_out/${TAG}_cfg3_full.txt
+    rm -f "$k" ;;
+  fbpre)
+    # the flag passes with the tile's positions loaded first (CRDT_SORTED_FORM bit 134217728): every flagged test with
+    # the bit set, then the flagged merge A/B (old / new) in one process under the kernel trace
+    CRDT_SORTED_FORM=134217728 timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "flagged" \
+      > gpurun_out/${TAG}_pytest_fbpre.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_fbpre.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_fbpre.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_fbpre
+    STEPS=12 AB=CRDT_SORTED_FORM=0,134217728 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d gpurun_out/${TAG}_prof_fbpre -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_fbpre.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_fbpre.log; [ $rc -eq 0 ] || exit $rc
+    k=$(find gpurun_out/${TAG}_prof_fbpre -name "*kernel_stats.csv" | head -1)
+    grep -i "flags_back\|pflags" "$k" | cut -c1-300
+    find gpurun_out/${TAG}_prof_fbpre -name "*kernel_trace.csv" -delete ;;
+  lists)
+    # round-6 closing forms: the flag passes with positions first (default; 134217728 = round 5's, 536870912 = level 2
+    # in 512-thread workgroups), the packed resolve's per-kernel item lists (default; 268435456 = every item slot);
+    # sorted / flagged / sparse parity, then A/Bs on the flagged merge (kernel trace), cfg3 and the fan-in
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "flagged or sorted or sparse or compact or scan_step or fused" \
+      > gpurun_out/${TAG}_pytest_lists.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_lists.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_lists.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_fb
+    STEPS=12 AB=CRDT_SORTED_FORM=0,134217728,536870912 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_fb -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_fb.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_fb.log; [ $rc -eq 0 ] || exit $rc
+    k=$(find gpurun_out/${TAG}_prof_fb -name "*kernel_stats.csv" | head -1)
+    grep -i "flags_back" "$k" | cut -c1-250
+    find gpurun_out/${TAG}_prof_fb -name "*kernel_trace.csv" -delete
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,268435456 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_lists_cfg3.json 2> gpurun_out/${TAG}_ab_lists_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_lists_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,268435456 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_lists.json 2> gpurun_out/${TAG}_ab_lists.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_lists.log; [ $rc -eq 0 ] || exit $rc
+    rm -rf gpurun_out/${TAG}_prof_cfg3
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg3 -o run \
+      -- python3 bench.py --config cfg3 --steps 5 --warmup 2 --no-cpu --no-pcie --no-census --flag-steps 0 \
+      > gpurun_out/${TAG}_prof_cfg3.json 2> gpurun_out/${TAG}_prof_cfg3.log
+    rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_prof_cfg3.log; exit $rc; }
+    k=$(find gpurun_out/${TAG}_prof_cfg3 -name "*kernel_trace.csv" | head -1)
+    python3 tools/ktrace_full.py "$k" > gpurun_out/${TAG}_cfg3_full.txt; head -26 gpurun_out/${TAG}_cfg3_full.txt
+    rm -f "$k" ;;
+  lists2)
+    # the ordered (flagged) resolve on item lists (default; 268435456 = every slot) and the level-1 flag pass staging
+    # 28 bytes per batch (1073741824): flagged parity, then the flagged merge A/B under the kernel trace
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "flagged or sorted_sparse or packed_form" \
+      > gpurun_out/${TAG}_pytest_lists2.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_lists2.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_lists2.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_fb
+    STEPS=12 AB=CRDT_SORTED_FORM=0,268435456,1073741824 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_fb -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_fb.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_fb.log; [ $rc -eq 0 ] || exit $rc
+    find gpurun_out/${TAG}_prof_fb -name "*kernel_trace.csv" -delete ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
