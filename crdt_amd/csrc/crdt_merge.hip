@@ -260,13 +260,13 @@ struct ScanHist {
 
 // kVec: a thread's records are 4 groups of 4 consecutive ones (lt read with two 16-B loads per
 // group, keys with one) instead of 16 strided ones; every per-tile result is order-free.
-template <bool kEager, bool kMillis = true, bool kFrame = false, bool kHist = false, bool kVec = false>
-__global__ __launch_bounds__(kScanThreads) void k_scan(
+template <bool kEager, bool kMillis, bool kFrame, bool kHist, bool kVec>
+__device__ __forceinline__ void scan_body(
     const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
     const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
     int64_t wall, uint32_t local_rank,
-    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh, bool jx = false)
+    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh, bool jx)
 {
     // (kFrame without kEager: the lt frame only — the host declared a rank bound, crdt_set_rank_bound)
     __shared__ int64_t s_max[kScanThreads / 64];
@@ -430,6 +430,18 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(
                 sh.hist[(uint64_t)(sh.ptb[j] + u * per + h) * 256 + threadIdx.x] = s_h[h * 256 + threadIdx.x];
       }
     }
+}
+
+template <bool kEager, bool kMillis = true, bool kFrame = false, bool kHist = false, bool kVec = false>
+__global__ __launch_bounds__(kScanThreads) void k_scan(
+    const int64_t* __restrict__ lt, const uint32_t* __restrict__ rank,
+    const int64_t* __restrict__ millis, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ tstart, uint32_t jbase, int64_t c0,
+    int64_t wall, uint32_t local_rank,
+    int64_t* __restrict__ T, Misc* __restrict__ misc, uint32_t* __restrict__ cand_tile, ScanHist sh, bool jx = false)
+{
+    scan_body<kEager, kMillis, kFrame, kHist, kVec>(lt, rank, millis, offs, tstart, jbase, c0, wall, local_rank, T, misc,
+                                                    cand_tile, sh, jx);
 }
 
 // M_j = max of changeset j's tile maxima (INT64_MIN when empty).  One block per changeset
@@ -1567,6 +1579,8 @@ constexpr uint32_t kFormFbackXcd = 1u << 21;
 constexpr uint32_t kFormFbackWide = 1u << 22;
 constexpr uint32_t kFormScanJx = 1u << 24;      // the clock scan's step-major grid (k_scan's jx) on every batch
 constexpr uint32_t kFormNoScanJx = 1u << 25;    // ... on none (default: batches of at most kScanJxMax workgroups)
+constexpr uint32_t kFormNoPosT = 1u << 31;      // flagged level 1: positions at the input index (LDS-staged), not
+                                                // tile-strided from registers (k_part_scatter1<.., kPT>)
 constexpr uint32_t kFormNoItemLists = 1u << 28; // the order-free packed resolve's kernels over every item slot
 constexpr uint32_t kFormNoFbackPre = 1u << 27;  // the flag passes of round 5 (k_flags_back), not k_flags_back_pre
 constexpr uint32_t kFormFbackPre512 = 1u << 29; // k_flags_back_pre's level-2 pass in 512-thread workgroups (not 256)
@@ -2473,7 +2487,12 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     c->last_key8 = k8;
     c->last_key16 = k16;
     c->last_hw = pk && (!c->counts || ord) && c->hw_read < c->cap;     // (in the first window)
-    if (fl) {
+    // flagged, compact, one window, the default level-1 flag pass: the level-1 positions tile-strided (kPT)
+    const uint32_t win0 = pk ? pf.jwin : kWindow;
+    const bool pt1 = fl && cmp && ns_all && sg.j[0] / win0 == sg.j[ns_all - 1] / win0 &&
+                     !(c->form_off & (kFormNoPosT | kFormNoFbackPre | kFormFbackWide)) &&
+                     !(c->xcd_map && (c->form_off & kFormFbackXcd));
+    if (fl && !pt1) {
         uint64_t ncol = 0;                                           // input index space of pos1
         for (size_t s = 0; s < ns_all; ++s) ncol = std::max<uint64_t>(ncol, sg.end[s]);
         HIPALLOC(c->f_pos1.ensure((ncol ? ncol : 1) + 8));   // + 8: k_flags_back_pre's clamped loads
@@ -2592,7 +2611,13 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
         if (c->place_timed && s0 == 0) HIPCHK(hipEventRecord(c->place_ev[0], c->stream));   // (the first window)
         const uint32_t xper1 = c->xcd_map ? (nt1 + kXcds - 1) / kXcds : 0;
         const bool rev1 = c->xcd_map && !(c->form_off & kFormNoReverse);
-        if (cmp && fl)          // the compact form's flagged level 1 (with positions)
+        if (pt1) HIPALLOC(c->f_pos1.ensure((size_t)nt1 * kPTile + 16));   // tile t's positions at t * kPTile
+        if (pt1)                // ... tile-strided, stored from registers
+            k_part_scatter1<true, false, true, kL1Items, true, true, true, true, true>
+                <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
+                cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
+                p1k, xper1, pf, rev1 ? hist1 : nullptr, c->f_pos1.p, hist1);
+        else if (cmp && fl)     // the compact form's flagged level 1 (with positions)
             k_part_scatter1<true, false, true, kL1Items, true, true, true, true>
                 <<<xcd_grid(nt1, c->xcd_map), kPThreads, 0, c->stream>>>(
                 cols.key, cols.lt, cols.rank, cols.val, tm1, jb, c->d_misc, c->cap, shift1, c->p_toff.p, p1r,
@@ -2907,7 +2932,10 @@ int apply_sorted(crdt_ctx* c, const Cols& cols, const Segs& sg, int64_t wall, co
     k_flags_back<true, CHK, kPTile, W><<<xcd_grid(nt1, fx1), 512, 0, c->stream>>>(                        \
         tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc, xf1)
             if (fl) {
-                if (!(c->form_off & (kFormNoFbackPre | kFormFbackWide)) && !fx1)
+                if (pt1)
+                    k_flags_back_pre<true, 6, kPTile, 14, 512, true><<<nt1, 512, 0, c->stream>>>(
+                        tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc);
+                else if (!(c->form_off & (kFormNoFbackPre | kFormFbackWide)) && !fx1)
                     k_flags_back_pre<true, 6, kPTile, 14><<<nt1, 512, 0, c->stream>>>(
                         tm1, hist1, c->p_toff.p, c->f_pos1.p, f1, dflags, c->d_misc);
                 else if (c->form_off & kFormFbackWide) { CRDT_FBACK1(6, true); }
@@ -3204,7 +3232,7 @@ static void read_env_knobs(crdt_ctx* c) {
     if (const char* e = getenv("CRDT_HIST_FUSE")) c->hist_fuse = atoi(e) != 0;
     if (const char* e = getenv("CRDT_L1_TILE"))
         c->l1_tile = std::min<uint32_t>((uint32_t)std::max(atoi(e), 0) / 1024u * 1024u, (uint32_t)kPTile);
-    if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)atoi(e);
+    if (const char* e = getenv("CRDT_SORTED_FORM")) c->form_off = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CRDT_APPLY_ITEMS")) {
         const int v = atoi(e);
         c->apply_items = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;

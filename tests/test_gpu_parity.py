@@ -1822,7 +1822,7 @@ def test_flagged_switch_off(gpu_device, monkeypatch):
 
 @pytest.mark.parametrize("chk,form", [("0", "134217728"), ("4", "134217728"), ("6", "134217728"), ("6", "0"),
                                       ("6", "4194304"), ("6", "2097152"), ("6", "8388608"), ("6", "14680064"),
-                                      ("6", "536870912"), ("6", "268435456")])
+                                      ("6", "536870912"), ("6", "268435456"), ("6", "2147483648")])
 def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, form):
     """The flag passes: round 5's one-byte staging (CRDT_SORTED_FORM bit 134217728) with its run search without
     checkpoints (CRDT_FBACK_CHK=0), one per 16 staged bytes (4) and one per 64 (6); the default k_flags_back_pre
@@ -1830,7 +1830,8 @@ def test_flagged_back_pass_search_forms(gpu_device, monkeypatch, chk, form):
     staging with eight-record gathers (4194304), the scatters' XCD tile order (2097152), the split buckets' fold
     and carry-ins on a side stream beside the unsplit buckets' walk (8388608), all three (14680064);
     k_flags_back_pre's level-2 pass in 512-thread workgroups (536870912); the fold and walk over every item slot
-    (268435456): split hot bucket, cold buckets on the 2-B level-1 key column, a late drift — same flags, rows and counts as the
+    (268435456); the level-1 positions at the input index, not tile-strided (2147483648): split hot bucket, cold
+    buckets on the 2-B level-1 key column, a late drift — same flags, rows and counts as the
     oracle."""
     monkeypatch.setenv("CRDT_FBACK_CHK", chk)
     monkeypatch.setenv("CRDT_SORTED_FORM", form)

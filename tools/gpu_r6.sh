@@ -198,6 +198,35 @@ case "${STAGE:-comm}" in
       --output-format csv -d gpurun_out/${TAG}_prof_fb -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_fb.log 2>&1
     rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_fb.log; [ $rc -eq 0 ] || exit $rc
     find gpurun_out/${TAG}_prof_fb -name "*kernel_trace.csv" -delete ;;
+  scanw5)
+    # the fused-histogram scan at 5 waves per SIMD (bit 1073741824): parity subset, A/B on the fan-in and cfg3; then
+    # cfg3's HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE passes, tools/gpu_pmc_cfg3.sh)
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "packed_form_switches or scan_step_major or sorted_compact" \
+      > gpurun_out/${TAG}_pytest_scanw5.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_scanw5.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_scanw5.log
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanw5.json 2> gpurun_out/${TAG}_ab_scanw5.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanw5.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanw5_cfg3.json 2> gpurun_out/${TAG}_ab_scanw5_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanw5_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_pmc_cfg3.sh || exit 1
+    python3 tools/pmc_kernels.py gpurun_out/pmc_cfg3/p1 gpurun_out/pmc_cfg3/p2 > gpurun_out/${TAG}_pmc_cfg3.txt 2>&1
+    rc=$?; cat gpurun_out/${TAG}_pmc_cfg3.txt; rm -rf gpurun_out/pmc_cfg3; exit $rc ;;
+  posT)
+    # the flagged level 1's tile-strided positions from registers (default; 2147483648 = LDS-staged at the input
+    # index): flagged parity, then the flagged merge A/B under the kernel trace
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "flagged" \
+      > gpurun_out/${TAG}_pytest_posT.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_posT.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_posT.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_posT
+    STEPS=12 AB=CRDT_SORTED_FORM=0,2147483648 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_posT -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_posT.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_posT.log; [ $rc -eq 0 ] || exit $rc
+    find gpurun_out/${TAG}_prof_posT -name "*kernel_trace.csv" -delete
+    k=$(find gpurun_out/${TAG}_prof_posT -name "*kernel_stats.csv" | head -1)
+    grep -i "flags_back\|scatter1" "$k" | cut -c1-200 ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
