@@ -227,6 +227,41 @@ case "${STAGE:-comm}" in
     find gpurun_out/${TAG}_prof_posT -name "*kernel_trace.csv" -delete
     k=$(find gpurun_out/${TAG}_prof_posT -name "*kernel_stats.csv" | head -1)
     grep -i "flags_back\|scatter1" "$k" | cut -c1-200 ;;
+  sparset)
+    # the sparse threshold re-tuned on the closing tree's cfg3 (k_resolve_sparse), then the default bench line
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 18 --warmup 2 --ab CRDT_SPARSE_T=2048,4096,8192 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_sparset_cfg3.json 2> gpurun_out/${TAG}_ab_sparset_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_sparset_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 420 python -u bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
+    rc=$?; tail -2 gpurun_out/${TAG}_bench_default.log; exit $rc ;;
+  hist4)
+    # the level-2 histogram with four tiles per workgroup (default; 1073741824 = one): parity subset, A/B on the fan-in,
+    # cfg3 and the flagged merge
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "packed_form_switches or sorted or compact or flagged_equals" \
+      > gpurun_out/${TAG}_pytest_hist4.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_hist4.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_hist4.log
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_hist4.json 2> gpurun_out/${TAG}_ab_hist4.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_hist4.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_hist4_cfg3.json 2> gpurun_out/${TAG}_ab_hist4_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_hist4_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_h4
+    STEPS=12 AB=CRDT_SORTED_FORM=0,1073741824 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_h4 -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_h4flags.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_h4flags.log; [ $rc -eq 0 ] || exit $rc
+    find gpurun_out/${TAG}_prof_h4 -name "*kernel_trace.csv" -delete
+    k=$(find gpurun_out/${TAG}_prof_h4 -name "*kernel_stats.csv" | head -1)
+    grep -i "hist16w" "$k" | cut -c1-160 ;;
+  spside)
+    # the sparse buckets on the side stream (1073741824) against the default: parity subset, cfg3 A/B
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "sparse or packed_form_switches" \
+      > gpurun_out/${TAG}_pytest_spside.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_spside.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_spside.log
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 20 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_spside_cfg3.json 2> gpurun_out/${TAG}_ab_spside_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_spside_cfg3.log; exit $rc ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
