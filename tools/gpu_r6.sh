@@ -262,6 +262,34 @@ case "${STAGE:-comm}" in
     timeout -k 10 300 python -u bench.py --config cfg3 --steps 20 --warmup 2 --ab CRDT_SORTED_FORM=0,1073741824 \
       --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_spside_cfg3.json 2> gpurun_out/${TAG}_ab_spside_cfg3.log
     rc=$?; grep "A/B" gpurun_out/${TAG}_ab_spside_cfg3.log; exit $rc ;;
+  closing)
+    # the closing tree's evidence: the default command under the kernel trace + its PMC bytes (r06_pmc_bench.json),
+    # the cfg3 line with full-table parity, then the driver's N = 8 command as 8 gloo ranks on this GPU
+    STAGE=profiles TAG=$TAG bash tools/gpu_r6.sh || exit 1
+    timeout -k 10 420 python -u bench.py --config cfg3 > gpurun_out/${TAG}_bench_cfg3.json 2> gpurun_out/${TAG}_bench_cfg3.log
+    rc=$?; tail -2 gpurun_out/${TAG}_bench_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    NS=8 TAG=${TAG}n8 LIMIT=600 bash tools/gpu_rehearse_n.sh ;;
+  libab)
+    # the tree's library against build_ab/libcrdt_prev.so (CRDT_LIB_PATH), alternating processes: the fan-in, cfg3
+    # and the flagged merge; parity subset on the tree's library first
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "sorted or compact or flagged" \
+      > gpurun_out/${TAG}_pytest_libab.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_libab.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_libab.log
+    for i in 1 2; do
+      for lib in tree prev; do
+        L=""; [ $lib = prev ] && L=$PWD/build_ab/libcrdt_prev.so
+        CRDT_LIB_PATH=$L timeout -k 10 300 python -u bench.py --steps 6 --warmup 2 --no-cpu --no-census --no-pcie \
+          --flag-steps 0 > gpurun_out/${TAG}_${lib}_$i.json 2> gpurun_out/${TAG}_${lib}_$i.log || exit 1
+        CRDT_LIB_PATH=$L timeout -k 10 300 python -u bench.py --config cfg3 --steps 12 --warmup 2 --no-cpu --no-census \
+          --no-pcie --flag-steps 0 > gpurun_out/${TAG}_${lib}_cfg3_$i.json 2> gpurun_out/${TAG}_${lib}_cfg3_$i.log || exit 1
+        CRDT_LIB_PATH=$L STEPS=6 timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_${lib}_flags_$i.log 2>&1 || exit 1
+        python3 -c "
+import json
+a=json.load(open('gpurun_out/${TAG}_${lib}_$i.json')); b=json.load(open('gpurun_out/${TAG}_${lib}_cfg3_$i.json'))
+f=[l for l in open('gpurun_out/${TAG}_${lib}_flags_$i.log') if l.startswith('A/B') or 'mean' in l]
+print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phases_ms_per_step'], 'cfg3', b['ms_per_step'], f[-1].strip() if f else '')"
+      done
+    done ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
