@@ -305,6 +305,20 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
     STEPS=12 AB=CRDT_SORTED_FORM=0,1073741824,4096 timeout -k 10 300 python -u tools/prof_flags.py \
       > gpurun_out/${TAG}_ab_scanacc_flags.log 2>&1
     rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_scanacc_flags.log; exit $rc ;;
+  scanpf)
+    # the sorted path's scan with the next tile in flight (k_scan_pf, default; 4096 = k_scan): parity subset, A/B on
+    # the fan-in, cfg3 and the flagged merge
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "packed_form_switches or sorted or compact or flagged or scan_step" \
+      > gpurun_out/${TAG}_pytest_scanpf.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_scanpf.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_scanpf.log
+    timeout -k 10 300 python -u bench.py --steps 12 --warmup 2 --ab CRDT_SORTED_FORM=0,4096 --no-cpu --no-census \
+      --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanpf.json 2> gpurun_out/${TAG}_ab_scanpf.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanpf.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 16 --warmup 2 --ab CRDT_SORTED_FORM=0,4096 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_scanpf_cfg3.json 2> gpurun_out/${TAG}_ab_scanpf_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanpf_cfg3.log; [ $rc -eq 0 ] || exit $rc
+    STEPS=12 AB=CRDT_SORTED_FORM=0,4096 timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_ab_scanpf_flags.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_scanpf_flags.log; exit $rc ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
