@@ -319,6 +319,14 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
     rc=$?; grep "A/B" gpurun_out/${TAG}_ab_scanpf_cfg3.log; [ $rc -eq 0 ] || exit $rc
     STEPS=12 AB=CRDT_SORTED_FORM=0,4096 timeout -k 10 300 python -u tools/prof_flags.py > gpurun_out/${TAG}_ab_scanpf_flags.log 2>&1
     rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_scanpf_flags.log; exit $rc ;;
+  cfgs)
+    # the other single-GPU configs on the closing tree, each with its parity: cfg2 (one 10M changeset), cfg5 (100
+    # streaming 10M-record deltas)
+    for cfg in cfg2 cfg5; do
+      timeout -k 10 420 python -u bench.py --config $cfg > gpurun_out/${TAG}_bench_$cfg.json 2> gpurun_out/${TAG}_bench_$cfg.log
+      rc=$?; tail -1 gpurun_out/${TAG}_bench_$cfg.log; [ $rc -eq 0 ] || exit $rc
+      python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_bench_$cfg.json')); print('$cfg', d['ms_per_step'], d['value'], d['roofline']['frac'], (d.get('parity') or {}).get('equal'))"
+    done ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
