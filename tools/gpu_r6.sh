@@ -327,6 +327,11 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
       rc=$?; tail -1 gpurun_out/${TAG}_bench_$cfg.log; [ $rc -eq 0 ] || exit $rc
       python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_bench_$cfg.json')); print('$cfg', d['ms_per_step'], d['value'], d['roofline']['frac'], (d.get('parity') or {}).get('equal'))"
     done ;;
+  cfg5jx)
+    # cfg5 with the scan's step-major grid (the default: its 10M-record deltas are ~2.4K workgroups) against forced off
+    timeout -k 10 420 python -u bench.py --config cfg5 --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,33554432 --no-cpu --no-census --no-pcie \
+      > gpurun_out/${TAG}_ab_cfg5jx.json 2> gpurun_out/${TAG}_ab_cfg5jx.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_cfg5jx.log; exit $rc ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
