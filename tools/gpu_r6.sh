@@ -332,6 +332,20 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
     timeout -k 10 420 python -u bench.py --config cfg5 --steps 8 --warmup 2 --ab CRDT_SORTED_FORM=0,33554432 --no-cpu --no-census --no-pcie \
       > gpurun_out/${TAG}_ab_cfg5jx.json 2> gpurun_out/${TAG}_ab_cfg5jx.log
     rc=$?; grep "A/B" gpurun_out/${TAG}_ab_cfg5jx.log; exit $rc ;;
+  fb1024)
+    # the level-1 flag pass in 1024-thread workgroups (bit 2) against 512: flagged parity, then the flagged merge A/B
+    # under the kernel trace
+    timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "flagged" \
+      > gpurun_out/${TAG}_pytest_fb1024.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_fb1024.log; exit 1; }
+    tail -2 gpurun_out/${TAG}_pytest_fb1024.log
+    export TMPDIR=/tmp
+    rm -rf gpurun_out/${TAG}_prof_fb
+    STEPS=12 AB=CRDT_SORTED_FORM=0,2 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d gpurun_out/${TAG}_prof_fb -o run -- python3 tools/prof_flags.py > gpurun_out/${TAG}_ab_fb1024.log 2>&1
+    rc=$?; grep "A/B\|DIFFER" gpurun_out/${TAG}_ab_fb1024.log; [ $rc -eq 0 ] || exit $rc
+    find gpurun_out/${TAG}_prof_fb -name "*kernel_trace.csv" -delete
+    k=$(find gpurun_out/${TAG}_prof_fb -name "*kernel_stats.csv" | head -1)
+    grep -i "flags_back" "$k" | cut -c1-200 ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
