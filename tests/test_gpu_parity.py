@@ -1964,3 +1964,28 @@ def test_sorted_compact_fanin_equals_oracle(gpu_device):
             t.close()
         finally:
             os.environ.pop("CRDT_SORTED_FORM", None)
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_sweep_sorted_forms(gpu_device, seed):
+    """Randomised sweep over the sorted path's round-6 forms at their defaults — compact keys, the step-major scan
+    grid, per-kernel item lists, sparse buckets in k_resolve_sparse, and (odd seeds) the flagged form with
+    k_flags_back_pre and tile-strided level-1 positions: random table sizes (one or two levels), changeset counts
+    and sizes, clock spans (ties to wide frames), node ranks, tombstones, invisible rows, duplicate-node and drift
+    records, explicit millis columns — every row, flag and exception field equal to the C oracle's."""
+    rng = np.random.default_rng(7000 + seed)
+    n_ids = int(rng.integers(2000, 200_000 if seed < 32 else 1_500_000))
+    n_local = int(n_ids * rng.uniform(0.3, 0.95))
+    kw = dict(seed=8000 + seed, R=int(rng.integers(1, 48)), per_cs=int(rng.integers(100, 20_000 if seed < 32 else 150_000)),
+              n_local=n_local, n_new=n_ids - n_local, millis_span=int(rng.choice([1, 8, 300, 70_000])),
+              counter_span=int(rng.integers(1, 6)), n_ranks=int(rng.integers(2, 60)),
+              tomb_frac=float(rng.choice([0.0, 0.2])), neg_mod_frac=float(rng.choice([0.0, 0.05])),
+              dup_frac=float(rng.choice([0.0, 0.0005])), drift_frac=float(rng.choice([0.0, 0.0005])),
+              explicit_millis=bool(rng.random() < 0.2))
+    kw["local_rank"] = int(rng.integers(0, kw["n_ranks"]))
+    case = make_case(**kw)
+    flagged = bool(seed % 2)
+    capacity = max(n_ids, (1 << 20) + 3) if seed % 3 == 0 else n_ids
+    res = compare_with_oracle(case, path="sorted", flags=flagged, counts=flagged, capacity=capacity,
+                              rank_bound=int(case["rank"].max()) + 1 if len(case["rank"]) else 0, device_cols=True)
+    assert res["path"] == "sorted"

@@ -346,6 +346,10 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
     find gpurun_out/${TAG}_prof_fb -name "*kernel_trace.csv" -delete
     k=$(find gpurun_out/${TAG}_prof_fb -name "*kernel_stats.csv" | head -1)
     grep -i "flags_back" "$k" | cut -c1-200 ;;
+  sweep)
+    timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "random_sweep" > gpurun_out/${TAG}_pytest_sweep.log 2>&1 \
+      || { tail -60 gpurun_out/${TAG}_pytest_sweep.log; exit 1; }
+    tail -3 gpurun_out/${TAG}_pytest_sweep.log ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
