@@ -350,6 +350,10 @@ print('$lib $i fanin', a['ms_per_step'], a['roofline']['dominant_kernel']['phase
     timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "random_sweep" > gpurun_out/${TAG}_pytest_sweep.log 2>&1 \
       || { tail -60 gpurun_out/${TAG}_pytest_sweep.log; exit 1; }
     tail -3 gpurun_out/${TAG}_pytest_sweep.log ;;
+  sparset2)
+    timeout -k 10 300 python -u bench.py --config cfg3 --steps 18 --warmup 2 --ab CRDT_SPARSE_T=2048,1024,1536 \
+      --no-cpu --no-census --no-pcie --flag-steps 0 > gpurun_out/${TAG}_ab_sparset2_cfg3.json 2> gpurun_out/${TAG}_ab_sparset2_cfg3.log
+    rc=$?; grep "A/B" gpurun_out/${TAG}_ab_sparset2_cfg3.log; exit $rc ;;
   flagsq)
     # SQ counters of the flag passes on the closing tree: the wait / issue breakdown (each counter
     # checked against rocprofv3 -L first), then the LDS / VALU pass of tools/gpu_pmc_flags.sh
